@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark of the MI355X Clay engine (BASELINE.json `metric`).
+
+Workload (BASELINE.json configs[1]): device-resident Slicer::encode of a batch of 1024 x 4 MiB
+synthetic objects (SplitMix64, seed 0x7A9E5EED ^ object id) with the production
+profile Clay(20,7,16), rotated 1 MB stripes; one "step" = one te_encode_batch_device call over
+the whole batch (all 20 slices incl. metadata written to HBM).  Multi-GPU (torchrun): objects
+are partitioned across ranks (per-GPU batches, weak scaling), no data-path collective.
+
+Also: --mode repair (config 3) and --mode decode (config 4, slices 0..12 erased).
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MiB = 1024 * 1024
+N = 20
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
+METRIC = "device-resident encode GiB/s, batched 4 MiB objects, 1 MI355X; % HBM peak"
+ALG_BYTES = {  # algorithmic HBM bytes per 4 MiB object
+    "encode": 4 * MiB + N * 715_048,
+    "repair": 16 * 71_500 + 715_048,
+    "decode": 7 * 715_048 + 4 * MiB,
+}
+
+
+def splitmix_fill(torch, out_u8, first_obj: int, nobj: int, obj_len: int, seed: int = 0x7A9E5EED):
+    """Device-side SplitMix64 stream per object: byte j of object i = word floor(j/8) of
+    SplitMix64(seed ^ i), little-endian.  Same stream as oracle.splitmix64_bytes."""
+    words = obj_len // 8
+    G = -7046029254386353131  # 0x9E3779B97F4A7C15 as int64
+    M1 = -4658895280553007687  # 0xBF58476D1CE4E5B9
+    M2 = -7723592293110705685  # 0x94D049BB133111EB
+    idx = torch.arange(1, words + 1, dtype=torch.int64, device=out_u8.device)
+
+    def lsr(x, k):
+        return (x >> k) & ((1 << (64 - k)) - 1)
+
+    for i in range(nobj):
+        s = (seed ^ (first_obj + i))
+        if s >= 1 << 63:
+            s -= 1 << 64
+        z = idx * G + s
+        z = (z ^ lsr(z, 30)) * M1
+        z = (z ^ lsr(z, 27)) * M2
+        z = z ^ lsr(z, 31)
+        out_u8[i * obj_len:i * obj_len + words * 8].copy_(z.view(torch.uint8))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--objects", type=int, default=1024, help="objects per GPU per step")
+    ap.add_argument("--object-bytes", type=int, default=4 * MiB)
+    ap.add_argument("--mode", choices=["encode", "repair", "decode"], default="encode")
+    ap.add_argument("--cpu-sample", type=int, default=96, help="objects in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity cores)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import tape_amd as T
+    from tape_amd import batch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+    T.lib.te_set_device(dev.index)
+
+    L, nobj = args.object_bytes, args.objects
+    slicer = T.Slicer.clay_default()
+    g = slicer.geometry(L)
+    per = N * g.slice_len
+    first = rank * nobj
+    d_in = torch.empty(nobj * L, dtype=torch.uint8, device=dev)
+    splitmix_fill(torch, d_in, first, nobj, L)
+    d_out = torch.empty(nobj * per, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    enc_objs = [(i * L, L, i * per, 0) for i in range(nobj)]
+
+    def encode_step():
+        batch.encode_batch(slicer, d_in, enc_objs, d_out, stream)
+
+    step = encode_step
+    unit_bytes = ALG_BYTES[args.mode] if L == 4 * MiB else None
+    if args.mode != "encode":
+        encode_step()
+        torch.cuda.synchronize()
+    if args.mode == "decode":
+        metas = b"".join(d_out[i * per + g.slice_len - 48:i * per + g.slice_len].cpu().numpy().tobytes()
+                         for i in range(nobj))
+        mask = sum(1 << j for j in range(13, 20))
+        dec_objs = [(i * per, g.slice_len, mask, i * L) for i in range(nobj)]
+        d_dec = torch.empty(nobj * L, dtype=torch.uint8, device=dev)
+
+        def step():
+            batch.decode_batch(slicer, d_out, dec_objs, metas, d_dec, stream)
+    elif args.mode == "repair":
+        host_out = d_out.cpu().numpy()
+        plans, blobs, offs, cur = [], [], [], 0
+        for i in range(nobj):
+            lost = i % N
+            avail = [j for j in range(N) if j != lost]
+            p = slicer.repair_plan_from_params(lost, avail, L, g.stripe_size)
+            o = {}
+            for h in avail:
+                b = T.extract_repair_data(host_out[i * per + h * g.slice_len:i * per + (h + 1) * g.slice_len].tobytes(),
+                                          p, h)
+                if b:
+                    o[h] = cur
+                    blobs.append(b)
+                    cur += len(b)
+            plans.append(p)
+            offs.append(o)
+        d_help = torch.from_numpy(np.frombuffer(b"".join(blobs), np.uint8).copy()).to(dev)
+        d_rep = torch.empty(nobj * g.slice_len, dtype=torch.uint8, device=dev)
+        rep_objs = [(plans[i], offs[i], i * g.slice_len,
+                     host_out[i * per + g.slice_len - 48:i * per + g.slice_len].tobytes()) for i in range(nobj)]
+        del host_out
+
+        def step():
+            batch.repair_batch(slicer.coder, d_help, rep_objs, d_rep, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    launch_ms = [a.elapsed_time(b) for a, b in ev]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_objs = nobj * world * args.steps
+    gib_s = total_objs * L / elapsed / 2**30
+    avg_launch_s = sum(launch_ms) / len(launch_ms) / 1e3
+    achieved = (unit_bytes or 0) * nobj / avg_launch_s / 1e9 if unit_bytes else None
+
+    cpu = None
+    if rank == 0 and args.cpu_sample > 0 and args.mode == "encode":
+        cpu = cpu_baseline(args, np, torch, d_in, d_out, per, L)
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("mode") == args.mode and tj.get("objects") == nobj:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    if rank == 0:
+        line = {
+            "metric": METRIC if args.mode == "encode" else f"device-resident {args.mode} GiB/s, batched 4 MiB objects, 1 MI355X",
+            "value": round(gib_s, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (SplitMix64 per object, seed 0x7A9E5EED ^ id), device-resident",
+            "config": {"workload": {"encode": "Slicer::encode", "repair": "Slicer::repair (lost = i mod 20)",
+                                    "decode": "Slicer::decode (slices 0..12 erased)"}[args.mode]
+                       + f" of {nobj} x {L} B objects per GPU, Clay(20,7,16) rotated, 1 MB stripes",
+                       "objects_per_gpu": nobj, "object_bytes": L, "profile": "clay(20,7,16)",
+                       "parallelism": f"objects partitioned over {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4) if achieved else None,
+                         "traffic": traffic,
+                         "alg_bytes_per_launch": unit_bytes * nobj if unit_bytes else None,
+                         "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, np, torch, d_in, d_out, per, L):
+    """Oracle (C restatement of lib/slicer's Slicer::encode) on the host cores, bounded sample of
+    the same workload; its outputs double as a bit-exact check of the GPU outputs."""
+    from oracle import oracle as O
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except Exception:
+        cores = os.cpu_count() or 1
+    thr = args.cpu_threads or max(1, min(16, cores))
+    m = min(args.cpu_sample, args.objects)
+    host_in = d_in[:m * L].cpu().numpy()
+    clay = O.OracleClay(20, 7, 16)
+    out = np.zeros(m * per, np.uint8)
+    t = time.perf_counter()
+    O.encode_many(clay, host_in, L, m, out, per, thr)
+    wall = time.perf_counter() - t
+    gpu = d_out[:m * per].cpu().numpy()
+    match = bool(np.array_equal(gpu, out))
+    one = host_in[:L]
+    t = time.perf_counter()
+    O.slicer_encode_np(clay, one)
+    single = time.perf_counter() - t
+    return {"value": round(m * L / wall / 2**30, 4), "unit": "GiB/s", "cores": thr, "kind": "port",
+            "sample": f"{m} x 4 MiB objects (first {m} of the batch), {thr} threads, one object per thread",
+            "single_thread_GiBps": round(L / single / 2**30, 4), "affinity_cores": cores,
+            "gpu_matches_oracle_on_sample": match}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,217 @@
+/*
+ * tape_ec.h -- C ABI of the MI355X-native Tapedrive erasure-coding engine (libtapeec.so).
+ *
+ * Drop-in boundary for the reference hot path `lib/slicer` (crate tape-slicer).  Every entry
+ * point below replaces one Rust item of lib/slicer's public surface (lib/slicer/src/lib.rs:15-27);
+ * the file:line it replaces is cited next to it.  The Rust binding a maintainer would add
+ * (an `extern "C"` block behind `ClayCoder`/`Slicer`) is shown in INTEGRATION.md.
+ *
+ * Conventions (mirroring the reference):
+ *   - plain pointers + sizes, caller-allocated outputs, int status (0 = ok), no exceptions;
+ *   - status codes map 1:1 onto EncodeError / DecodeError / RepairError
+ *     (lib/slicer/src/errors.rs:5-37) plus engine errors;
+ *   - all GF(2^8) compute runs on the GPU (gfx950).  With no HIP device the compute entry
+ *     points return TE_ERR_NO_DEVICE: there is NO CPU fallback in this library.
+ *   - host-only entry points (geometry, metadata, rotation maps, repair planning, helper-side
+ *     gather) are pure integer bookkeeping and work without a GPU, as in the reference.
+ *   - thread safety: a te_clay may be used from several threads; calls on one te_clay are
+ *     serialised internally.  The GPU context is a process-wide singleton.
+ */
+#ifndef TAPE_EC_H
+#define TAPE_EC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TE_META_SIZE 48      /* SliceMetadata::SIZE          lib/slicer/src/metadata.rs:44 */
+#define TE_ROTATION_STEP 7   /* ROTATION_STEP                lib/slicer/src/slicer.rs:21   */
+#define TE_GROUP_SIZE 20     /* GROUP_SIZE                   lib/core/src/erasure.rs:5     */
+#define TE_ENCODING_CLAY 2   /* EncodingType::Clay           lib/core/src/encoding.rs:25   */
+#define TE_CLAY_DEFAULT_PARAMS 0x100714ull /* ClayParams::DEFAULT (20,7,16) encoding.rs:236-239 */
+
+typedef enum te_status {
+    TE_OK = 0,
+    /* EncodeError  errors.rs:5-11 */
+    TE_ERR_TOO_MUCH_DATA = 1,
+    TE_ERR_EMPTY_INPUT = 2,
+    /* DecodeError  errors.rs:13-23 */
+    TE_ERR_NOT_ENOUGH_SLICES = 3,
+    TE_ERR_BAD_ENCODING = 4,
+    TE_ERR_INVALID_LAYOUT = 5,
+    /* RepairError  errors.rs:25-37 */
+    TE_ERR_NOT_ENOUGH_HELPERS = 6,
+    TE_ERR_INVALID_SLICE = 7,
+    TE_ERR_CLAY = 8,
+    TE_ERR_MISSING_HELPER = 9,
+    /* engine */
+    TE_ERR_INVALID_ARG = 20,
+    TE_ERR_NO_DEVICE = 21,
+    TE_ERR_HIP = 22,
+    TE_ERR_UNSUPPORTED = 23,
+    TE_ERR_OUT_OF_MEMORY = 24,
+    TE_ERR_BUFFER_TOO_SMALL = 25
+} te_status;
+
+const char *te_strerror(int status);
+/* Number of usable gfx950 devices (0 on a CPU-only host).  Does not create a context. */
+int te_device_count(void);
+/* Bind the calling thread's engine context to a HIP device (default 0). */
+int te_set_device(int device);
+/* Library build identification string. */
+const char *te_version(void);
+
+/* ------------------------------------------------------------------------------------------
+ * ClayCoder                                                     lib/slicer/src/clay.rs:13-122
+ * ------------------------------------------------------------------------------------------ */
+typedef struct te_clay te_clay;
+typedef struct te_clay_info {
+    uint32_t n, k, m, d;     /* ErasureCoder::{n,k,m}, ClayCoder::d()   coder.rs:16-25, clay.rs:43-45 */
+    uint32_t q, t, nu;       /* Clay layout: q = d-k+1, t = (n+nu)/q                                */
+    uint32_t alpha, beta;    /* ClayCoder::alpha()/beta()                clay.rs:48-57              */
+} te_clay_info;
+
+/* ClayCoder::new(n, k, d)  clay.rs:24-34.  The reference panics on invalid params; this returns
+ * TE_ERR_INVALID_ARG.  Profiles whose layout the GPU engine does not cover return
+ * TE_ERR_UNSUPPORTED. */
+int te_clay_new(uint32_t n, uint32_t k, uint32_t d, te_clay **out);
+/* ClayCoder::from_params(ClayParams)  clay.rs:37-39 (packed n | k<<8 | d<<16, encoding.rs:193-197) */
+int te_clay_from_params(uint64_t packed_params, te_clay **out);
+void te_clay_free(te_clay *c);
+int te_clay_get_info(const te_clay *c, te_clay_info *out);
+/* ClayCoder::chunk_size_for  clay.rs:61-73 */
+size_t te_clay_chunk_size_for(const te_clay *c, size_t input_len);
+/* ClayCoder::track_chunk_size  clay.rs:81-84 */
+size_t te_clay_track_chunk_size(const te_clay *c, size_t stripe_size, size_t blob_len);
+/* ErasureCoder::encode for ClayCoder  clay.rs:99-104.  chunks: n*chunk_size bytes, chunk i at
+ * i*chunk_size.  Empty input -> TE_ERR_EMPTY_INPUT.  (GPU) */
+int te_clay_encode(te_clay *c, const uint8_t *data, size_t len, uint8_t *chunks, size_t cap,
+                   size_t *chunk_size);
+/* ErasureCoder::decode for ClayCoder  clay.rs:106-122.  chunks[i] == NULL marks chunk i missing.
+ * out: k*chunk_size bytes (padded data; the Slicer trims).  (GPU) */
+int te_clay_decode(te_clay *c, const uint8_t *const *chunks, size_t chunk_size, uint8_t *out,
+                   size_t cap);
+/* ClayCoder::plan_repair  repair.rs:53-70: helpers_out gets d shard ids (ascending),
+ * sub_chunks_out gets beta plane indices (ascending).  Host only. */
+int te_clay_plan_repair(const te_clay *c, uint32_t lost, const uint32_t *available, size_t navail,
+                        uint32_t *helpers_out, uint32_t *sub_chunks_out);
+/* ClayCoder::repair  repair.rs:75-88: helper_data[j] = beta*sub_chunk bytes of helpers[j].
+ * out = chunk_size bytes.  (GPU) */
+int te_clay_repair(te_clay *c, uint32_t lost, const uint32_t *helpers,
+                   const uint8_t *const *helper_data, size_t nhelpers, size_t chunk_size,
+                   uint8_t *out);
+
+/* ------------------------------------------------------------------------------------------
+ * Slicer<ClayCoder>                          lib/slicer/src/{adaptive,slicer,metadata}.rs
+ * ------------------------------------------------------------------------------------------ */
+size_t te_pick_stripe_size(size_t blob_len);                      /* adaptive.rs:31-39 */
+size_t te_num_stripes(size_t blob_len, size_t stripe_size);       /* adaptive.rs:43-49 */
+uint32_t te_shard_to_slice(int rotated, uint32_t n, uint32_t stripe, uint32_t shard); /* slicer.rs:34-42 */
+uint32_t te_slice_to_shard(int rotated, uint32_t n, uint32_t stripe, uint32_t slice); /* slicer.rs:46-54 */
+
+typedef struct te_slice_metadata {   /* SliceMetadata, 48-byte LE suffix   metadata.rs:22-37 */
+    uint64_t version, blob_len, stripe_size, encoding, params, chunk_index;
+} te_slice_metadata;
+/* SliceMetadata::to_bytes  metadata.rs:66-69 */
+void te_slice_metadata_to_bytes(const te_slice_metadata *m, uint8_t out[TE_META_SIZE]);
+/* SliceMetadata::from_slice  metadata.rs:72-87 (rejects stripe sizes not in STRIPE_SIZES) */
+int te_slice_metadata_from_slice(const uint8_t *slice, size_t len, te_slice_metadata *out);
+
+typedef struct te_slicer_cfg {       /* Slicer fields   slicer.rs:124-132 */
+    int rotated;                     /* MappingStrategy::Rotated if non-zero */
+    uint64_t encoding, params;       /* EncodingProfile written to the metadata suffix */
+    uint64_t chunk_index;            /* ChunkNumber salt */
+} te_slicer_cfg;
+typedef struct te_geometry {
+    uint64_t stripe_size, num_stripes, chunk_size, sub_chunk_size, slice_len;
+} te_geometry;
+/* Slicer::encode geometry (pick_stripe_size + chunk_size_for + metadata) slicer.rs:237-262 */
+int te_slicer_geometry(const te_clay *c, size_t blob_len, te_geometry *out);
+/* Slicer::encode  slicer.rs:237-296 (+ encode_empty_blob :368-387).  slices: n*slice_len
+ * bytes, slice i at i*slice_len.  (GPU) */
+int te_slicer_encode(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *data, size_t len,
+                     uint8_t *slices, size_t cap);
+/* Slicer::decode  slicer.rs:298-364.  slices[i] == NULL marks slice i missing; all present
+ * slices are slice_len bytes.  (GPU) */
+int te_slicer_decode(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *const *slices,
+                     size_t slice_len, uint8_t *out, size_t cap, size_t *out_len);
+
+/* ------------------------------------------------------------------------------------------
+ * Repair                                                       lib/slicer/src/repair.rs
+ * ------------------------------------------------------------------------------------------ */
+typedef struct te_repair_plan te_repair_plan;
+typedef struct te_repair_plan_info {  /* RepairPlan  repair.rs:16-28 */
+    uint32_t lost, num_stripes, d, beta;
+    uint64_t chunk_size, sub_chunk_size;
+} te_repair_plan_info;
+/* Slicer::repair_plan_from_params  repair.rs:137-201 (host only) */
+int te_repair_plan_from_params(const te_clay *c, int rotated, uint32_t lost,
+                               const uint32_t *available, size_t navail, uint64_t blob_len,
+                               uint64_t stripe_size, te_repair_plan **out);
+/* Slicer::repair_plan  repair.rs:208-281 (layout from a reference slice; host only) */
+int te_repair_plan_from_slice(const te_clay *c, int rotated, uint32_t lost,
+                              const uint32_t *available, size_t navail,
+                              const uint8_t *reference, size_t ref_len, te_repair_plan **out);
+void te_repair_plan_free(te_repair_plan *p);
+int te_repair_plan_get_info(const te_repair_plan *p, te_repair_plan_info *out);
+/* StripeRepair/HelperPlan  repair.rs:30-47: helper_slices/helper_shards get d entries,
+ * sub_chunks gets d*beta entries (helper-major). */
+int te_repair_plan_stripe(const te_repair_plan *p, uint32_t stripe, uint32_t *lost_shard,
+                          uint32_t *helper_slices, uint32_t *helper_shards, uint32_t *sub_chunks);
+/* Bytes helper `slice` contributes under the plan. */
+size_t te_extract_repair_data_size(const te_repair_plan *p, uint32_t helper_slice);
+/* extract_repair_data  repair.rs:97-130 (helper-side gather; host only) */
+int te_extract_repair_data(const te_repair_plan *p, const uint8_t *slice, size_t slice_len,
+                           uint32_t helper_slice, uint8_t *out, size_t cap, size_t *out_len);
+/* Slicer::repair  repair.rs:324-367: helper_data/helper_lens indexed by SLICE id (n entries,
+ * NULL = not provided).  out = num_stripes*chunk_size + 48 bytes.  (GPU) */
+int te_slicer_repair(te_clay *c, const te_repair_plan *p, const uint8_t *const *helper_data,
+                     const size_t *helper_lens, const uint8_t metadata[TE_META_SIZE],
+                     uint8_t *out, size_t cap);
+
+/* ------------------------------------------------------------------------------------------
+ * Device-resident batch API (new; the batching seam of sdk/src/stream/write.rs:332-362 and
+ * network/node/src/features/spool/repair.rs:94-226).  All pointers are DEVICE pointers;
+ * descriptors are host arrays; work is enqueued on `hip_stream` (NULL = default stream) and
+ * the call returns without synchronising.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct te_object {
+    uint64_t data_off;    /* object bytes at d_data + data_off */
+    uint64_t blob_len;
+    uint64_t out_off;     /* n slices at d_out + out_off, slice i at + i*slice_len */
+    uint64_t chunk_index;
+} te_object;
+/* Batched Slicer::encode of nobj objects (each object's geometry from its blob_len). */
+int te_encode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data,
+                           const te_object *objs, size_t nobj, uint8_t *d_out, void *hip_stream);
+
+typedef struct te_decode_object {
+    uint64_t slices_off;  /* slice i at d_slices + slices_off + i*slice_len */
+    uint64_t slice_len;
+    uint32_t avail_mask;  /* bit i set = slice i present */
+    uint32_t pad_;
+    uint64_t out_off;     /* blob bytes written at d_out + out_off */
+} te_decode_object;
+/* Batched Slicer::decode.  Metadata is read on the host from `h_meta` (nobj*48 bytes: one
+ * suffix per object, as the caller already holds them); no device->host sync is needed. */
+int te_decode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices,
+                           const te_decode_object *objs, const uint8_t *h_meta, size_t nobj,
+                           uint8_t *d_out, void *hip_stream);
+
+typedef struct te_repair_object {
+    const te_repair_plan *plan;
+    uint64_t helper_off[TE_GROUP_SIZE]; /* extract_repair_data output of slice i at d_helpers+off */
+    uint64_t out_off;                   /* num_stripes*chunk_size + 48 bytes at d_out + out_off */
+    uint8_t metadata[TE_META_SIZE];
+} te_repair_object;
+/* Batched Slicer::repair of nobj lost slices (each with its own plan). */
+int te_repair_batch_device(te_clay *c, const uint8_t *d_helpers, const te_repair_object *objs,
+                           size_t nobj, uint8_t *d_out, void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TAPE_EC_H */

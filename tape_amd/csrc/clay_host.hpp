@@ -1,0 +1,222 @@
+// clay_host.hpp -- host-side Clay layout math: node/plane geometry, repair planning and the
+// erasure-pattern tables the GPU engines consume.  Pure integer bookkeeping (the reference's
+// clay_codes::ClayCode::{new, minimum_to_repair} and the layered-decode ordering).
+#pragma once
+#include <stdint.h>
+#include <stddef.h>
+#include <vector>
+#include <algorithm>
+#include "kernels.hpp"
+
+namespace tec {
+
+struct ClayHost {
+    int n = 0, k = 0, m = 0, d = 0, q = 0, t = 0, nu = 0, qt = 0, alpha = 0, beta = 0;
+    Mat G;                       // qt x (k+nu) systematic generator (A2)
+    std::vector<uint32_t> qpow;  // q^i, i <= t
+
+    // ClayCoder::new asserts (clay.rs:24-34) + layout limits of the GPU engines.
+    // returns 0 ok, -1 invalid params, -2 unsupported layout.
+    int init(int n_, int k_, int d_) {
+        if (!(n_ > k_ && k_ > 0 && d_ >= k_ + 1 && d_ <= n_ - 1)) return -1;
+        n = n_; k = k_; m = n_ - k_; d = d_;
+        q = d - k + 1;
+        nu = (q - (n % q)) % q;
+        t = (n + nu) / q;
+        qt = q * t;
+        if (qt > kMaxNodes || qt > 64 || t >= 16) return -2;
+        long a = 1;
+        for (int i = 0; i < t; i++) {
+            a *= q;
+            if (a > 4096) return -2;
+        }
+        alpha = (int)a;
+        beta = alpha / q;
+        if (m > kGpeMaxErased || k + nu > kGpeMaxKnown) return -2;
+        // LDS budget of the generic engine: 2 * m * alpha words of 16 B per block
+        if ((size_t)2 * m * alpha * kGpeWords * 4 + (size_t)alpha * t > 150 * 1024) return -2;
+        G = rs_generator(k + nu, qt);
+        qpow.assign(16, 0);
+        uint32_t p = 1;
+        for (int i = 0; i <= t && i < 16; i++) { qpow[i] = p; p *= (uint32_t)q; }
+        return 0;
+    }
+
+    int ext_to_int(int e) const { return e < k ? e : e + nu; }
+    int int_to_ext(int i) const { return i < k ? i : (i < k + nu ? -1 : i - nu); }
+    int digit(int z, int y) const { return (int)((uint32_t)z / qpow[t - 1 - y] % (uint32_t)q); }
+
+    // ClayCoder::chunk_size_for  clay.rs:61-73
+    size_t chunk_size_for(size_t len) const {
+        const size_t min_size = (size_t)k * alpha * 2;
+        size_t padded = len == 0 ? min_size : ((len + min_size - 1) / min_size) * min_size;
+        if (padded < min_size) padded = min_size;
+        return padded / k;
+    }
+
+    // get_repair_subchunks, expanded ascending (A6)
+    std::vector<int> repair_planes(int lost_ext) const {
+        const int lost = ext_to_int(lost_ext);
+        const int y = lost / q, x = lost % q;
+        const int seq = (int)qpow[t - 1 - y], nseq = (int)qpow[y];
+        std::vector<int> out;
+        int index = x * seq;
+        for (int s = 0; s < nseq; s++) {
+            for (int j = index; j < index + seq; j++) out.push_back(j);
+            index += q * seq;
+        }
+        return out;
+    }
+
+    // minimum_to_repair (A6): column-mates of the lost node, then ascending available ids.
+    // returns 0 and d helper ext ids (ascending), or -1 (not enough helpers), -2 (column-mate
+    // unavailable / bad index).
+    int min_to_repair(int lost_ext, const std::vector<int> &avail, std::vector<int> &helpers) const {
+        if (lost_ext < 0 || lost_ext >= n) return -2;
+        if ((int)avail.size() < d) return -1;
+        std::vector<char> isav(n, 0), chosen(n, 0);
+        for (int a : avail)
+            if (a >= 0 && a < n) isav[a] = 1;
+        const int lost = ext_to_int(lost_ext);
+        int cnt = 0;
+        for (int j = 0; j < q; j++) {
+            if (j == lost % q) continue;
+            const int e = int_to_ext((lost / q) * q + j);
+            if (e < 0) continue;
+            if (!isav[e]) return -2;
+            if (!chosen[e]) { chosen[e] = 1; cnt++; }
+        }
+        for (int id = 0; id < n && cnt < d; id++)
+            if (isav[id] && !chosen[id] && id != lost_ext) { chosen[id] = 1; cnt++; }
+        if (cnt != d) return -1;
+        helpers.clear();
+        for (int id = 0; id < n; id++)
+            if (chosen[id]) helpers.push_back(id);
+        return 0;
+    }
+
+    // MDS decoding matrix for an internal erased set of size m: D = G_E * inv(G_known).
+    bool decoder(uint64_t erased_mask, std::vector<int> &known, std::vector<int> &erased, Mat &D) const {
+        const int kk = k + nu;
+        known.clear();
+        erased.clear();
+        for (int i = 0; i < qt; i++) {
+            if ((erased_mask >> i) & 1ull) erased.push_back(i);
+            else if ((int)known.size() < kk) known.push_back(i);
+        }
+        if ((int)known.size() != kk) return false;
+        Mat sub{};
+        sub.rows = sub.cols = kk;
+        for (int r = 0; r < kk; r++)
+            for (int c = 0; c < kk; c++) sub.v[r][c] = G.v[known[r]][c];
+        if (!mat_invert(sub)) return false;
+        D = Mat{};
+        D.rows = (int)erased.size();
+        D.cols = kk;
+        for (size_t e = 0; e < erased.size(); e++)
+            for (int j = 0; j < kk; j++) {
+                uint8_t acc = 0;
+                for (int l = 0; l < kk; l++) acc ^= gf_mul(G.v[erased[e]][l], sub.v[l][j]);
+                D.v[e][j] = acc;
+            }
+        return true;
+    }
+
+    // A7: pad an internal erased set with the lowest parity nodes until it has m members.
+    uint64_t pad_erasures(uint64_t mask) const {
+        int cnt = __builtin_popcountll(mask);
+        for (int i = k + nu; cnt < m && i < qt; i++)
+            if (!((mask >> i) & 1ull)) { mask |= 1ull << i; cnt++; }
+        return mask;
+    }
+
+    // Layered-decode pattern for the generic engine.  planes: appended to `pool`.
+    bool gpe_pattern(uint64_t erased_mask, GpePattern &P, std::vector<uint16_t> &pool) const {
+        std::vector<int> known, erased;
+        Mat D;
+        if (!decoder(erased_mask, known, erased, D)) return false;
+        P = GpePattern{};
+        P.erased_mask = erased_mask;
+        P.nknown = (uint32_t)known.size();
+        P.nerased = (uint32_t)erased.size();
+        P.alpha = (uint32_t)alpha;
+        for (size_t i = 0; i < known.size(); i++) P.known[i] = (uint8_t)known[i];
+        for (size_t i = 0; i < erased.size(); i++) P.erased[i] = (uint8_t)erased[i];
+        for (size_t e = 0; e < erased.size(); e++)
+            for (size_t j = 0; j < known.size(); j++) P.D[e][j] = perm_tab(D.v[e][j]);
+        std::vector<int> score(alpha, 0);
+        int maxs = 0;
+        for (int z = 0; z < alpha; z++) {
+            int s = 0;
+            for (int y = 0; y < t; y++)
+                if ((erased_mask >> (y * q + digit(z, y))) & 1ull) s++;
+            score[z] = s;
+            maxs = std::max(maxs, s);
+        }
+        if (maxs + 2 > 16) return false;
+        P.planes_off = (uint32_t)pool.size();
+        P.nlevels = (uint32_t)maxs + 1;
+        for (int L = 0; L <= maxs; L++) {
+            P.level_start[L] = (uint32_t)(pool.size() - P.planes_off);
+            for (int z = 0; z < alpha; z++)
+                if (score[z] == L) pool.push_back((uint16_t)z);
+        }
+        P.level_start[maxs + 1] = (uint32_t)(pool.size() - P.planes_off);
+        return true;
+    }
+
+    // Repair pattern (Ceph repair_one_lost_chunk): erased = lost column + aloof nodes.
+    bool rep_pattern(int lost_ext, const std::vector<int> &helpers_ext, RepPattern &P,
+                     std::vector<uint16_t> &pool, std::vector<uint16_t> &pind) const {
+        const int lost = ext_to_int(lost_ext);
+        std::vector<char> is_helper(qt, 0);
+        for (int h : helpers_ext) is_helper[ext_to_int(h)] = 1;
+        uint64_t aloof = 0, emask = 0;
+        for (int e = 0; e < n; e++) {
+            const int i = ext_to_int(e);
+            if (!is_helper[i] && e != lost_ext) aloof |= 1ull << i;
+        }
+        for (int i = 0; i < q; i++) emask |= 1ull << (lost - lost % q + i);
+        emask |= aloof;
+        if (__builtin_popcountll(emask) != m) return false;
+        std::vector<int> known, erased;
+        Mat D;
+        if (!decoder(emask, known, erased, D)) return false;
+        P = RepPattern{};
+        P.erased_mask = emask;
+        P.aloof_mask = aloof;
+        P.nknown = (uint32_t)known.size();
+        P.nerased = (uint32_t)erased.size();
+        P.beta = (uint32_t)beta;
+        P.lost = (uint32_t)lost;
+        for (size_t i = 0; i < known.size(); i++) P.known[i] = (uint8_t)known[i];
+        for (size_t i = 0; i < erased.size(); i++) P.erased[i] = (uint8_t)erased[i];
+        for (size_t e = 0; e < erased.size(); e++)
+            for (size_t j = 0; j < known.size(); j++) P.D[e][j] = perm_tab(D.v[e][j]);
+        const std::vector<int> rp = repair_planes(lost_ext);
+        const size_t base = pind.size();
+        pind.resize(base + alpha, 0xffff);
+        for (size_t i = 0; i < rp.size(); i++) pind[base + rp[i]] = (uint16_t)i;
+        std::vector<int> order(rp.size());
+        int maxo = 0;
+        for (size_t i = 0; i < rp.size(); i++) {
+            int o = 0;
+            for (int nd = 0; nd < qt; nd++)
+                if ((((aloof >> nd) & 1ull) || nd == lost) && digit(rp[i], nd / q) == nd % q) o++;
+            order[i] = o;
+            maxo = std::max(maxo, o);
+        }
+        if (maxo + 2 > 16) return false;
+        P.planes_off = (uint32_t)pool.size();
+        P.nlevels = (uint32_t)maxo + 1;
+        for (int L = 0; L <= maxo; L++) {
+            P.level_start[L] = (uint32_t)(pool.size() - P.planes_off);
+            for (size_t i = 0; i < rp.size(); i++)
+                if (order[i] == L) pool.push_back((uint16_t)rp[i]);
+        }
+        P.level_start[maxo + 1] = (uint32_t)(pool.size() - P.planes_off);
+        return true;
+    }
+};
+
+}  // namespace tec

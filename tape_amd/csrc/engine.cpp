@@ -1,0 +1,1020 @@
+// engine.cpp -- libtapeec.so: the C ABI (include/tape_ec.h) over the gfx950 Clay engines.
+//
+// Host side of the drop-in for lib/slicer: Slicer striping/padding/rotation/metadata
+// (slicer.rs, adaptive.rs, metadata.rs), repair planning (repair.rs), descriptor building and
+// launch orchestration.  All GF(2^8) arithmetic runs in the HIP kernels (encode_rows.hip,
+// gpe.hip); there is no CPU compute fallback -- without a device the compute calls fail with
+// TE_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+#include <string.h>
+#include <stdlib.h>
+#include <map>
+#include <mutex>
+#include <vector>
+#include <algorithm>
+#include "../../include/tape_ec.h"
+#include "kernels.hpp"
+#include "clay_host.hpp"
+
+using namespace tec;
+
+namespace {
+
+constexpr size_t kStripeSizes[3] = {100000, 1000000, 10000000};  // adaptive.rs:15-19
+
+int hip_status(hipError_t e) {
+    if (e == hipSuccess) return TE_OK;
+    if (e == hipErrorOutOfMemory) return TE_ERR_OUT_OF_MEMORY;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return TE_ERR_NO_DEVICE;
+    return TE_ERR_HIP;
+}
+
+#define TE_HIP(expr)                              \
+    do {                                          \
+        hipError_t e_ = (expr);                   \
+        if (e_ != hipSuccess) return hip_status(e_); \
+    } while (0)
+
+int g_device_count = -1;
+std::mutex g_dev_mu;
+
+int device_count() {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if (g_device_count < 0) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        g_device_count = n;
+    }
+    return g_device_count;
+}
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            if (e != hipSuccess) return e;
+            p = nullptr;
+            cap = 0;
+        }
+        size_t want = std::max<size_t>(n, 4096);
+        want = (want + 4095) & ~(size_t)4095;
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) { p = nullptr; return e; }
+        cap = want;
+        return hipSuccess;
+    }
+    template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct HostBuf {  // pinned staging for descriptor uploads
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 4096);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e != hipSuccess) { p = nullptr; return e; }
+        cap = want;
+        return hipSuccess;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// A descriptor arena: host image assembled per call, uploaded (only if changed) to a device
+// mirror on the caller's stream.  An event guards the pinned staging against reuse while a
+// previous upload may still be pending.
+struct Arena {
+    std::vector<uint8_t> img, last;
+    HostBuf stage;
+    DevBuf dev;
+    hipEvent_t ev = nullptr;
+    bool ev_pending = false;
+    hipStream_t last_stream = nullptr;
+    hipEvent_t done = nullptr;  // recorded after the launches that read `dev`
+    bool done_pending = false;
+
+    size_t put(const void *src, size_t bytes, size_t align = 16) {
+        size_t off = (img.size() + align - 1) & ~(align - 1);
+        img.resize(off + bytes);
+        if (bytes) memcpy(img.data() + off, src, bytes);
+        return off;
+    }
+    int upload(hipStream_t s) {
+        if (!ev) TE_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        if (!done) TE_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        if (img == last && dev.p && dev.cap >= img.size()) return TE_OK;
+        // device mirror may still be read by launches on another stream
+        if (done_pending && last_stream != s) TE_HIP(hipStreamWaitEvent(s, done, 0));
+        if (ev_pending) TE_HIP(hipEventSynchronize(ev));
+        ev_pending = false;
+        if (img.size() > dev.cap) {
+            // old mirror may still be referenced by queued kernels: drain before freeing
+            if (done_pending) TE_HIP(hipEventSynchronize(done));
+            TE_HIP(dev.ensure(img.size()));
+        }
+        TE_HIP(stage.ensure(img.size()));
+        memcpy(stage.p, img.data(), img.size());
+        TE_HIP(hipMemcpyAsync(dev.p, stage.p, img.size(), hipMemcpyHostToDevice, s));
+        TE_HIP(hipEventRecord(ev, s));
+        ev_pending = true;
+        last = img;
+        return TE_OK;
+    }
+    int mark_done(hipStream_t s) {
+        TE_HIP(hipEventRecord(done, s));
+        done_pending = true;
+        last_stream = s;
+        return TE_OK;
+    }
+    template <class T> const T *at(size_t off) const { return reinterpret_cast<const T *>(dev.as<uint8_t>() + off); }
+    void release() {
+        dev.release();
+        stage.release();
+        if (ev) (void)hipEventDestroy(ev);
+        if (done) (void)hipEventDestroy(done);
+        ev = done = nullptr;
+    }
+};
+
+void put_u64(uint8_t *p, uint64_t v) {
+    for (int i = 0; i < 8; i++) p[i] = (uint8_t)(v >> (8 * i));
+}
+uint64_t get_u64(const uint8_t *p) {
+    uint64_t v = 0;
+    for (int i = 0; i < 8; i++) v |= (uint64_t)p[i] << (8 * i);
+    return v;
+}
+
+bool valid_stripe(uint64_t s) { return s == kStripeSizes[0] || s == kStripeSizes[1] || s == kStripeSizes[2]; }
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+struct te_clay {
+    ClayHost h;
+    bool fast_encode = false;
+    std::mutex mu;
+    int device = 0;
+    hipStream_t stream = nullptr;  // for the synchronous host-buffer entry points
+    Arena enc, dec, rep;
+    DevBuf io_in, io_out;          // staging for host-buffer entry points
+};
+
+struct te_repair_plan {
+    uint32_t lost = 0, ns = 0, d = 0, beta = 0, n = 0;
+    uint64_t cs = 0, sc = 0;
+    std::vector<uint32_t> lost_shard;   // [ns]
+    std::vector<uint32_t> helper_slice; // [ns*d]
+    std::vector<uint32_t> helper_shard; // [ns*d]
+    std::vector<uint32_t> sub_chunks;   // [ns*d*beta]
+};
+
+extern "C" {
+
+const char *te_strerror(int s) {
+    switch (s) {
+        case TE_OK: return "ok";
+        case TE_ERR_TOO_MUCH_DATA: return "too much data to encode in a single stripe/coder configuration";
+        case TE_ERR_EMPTY_INPUT: return "empty input data";
+        case TE_ERR_NOT_ENOUGH_SLICES: return "not enough slices to reconstruct (need at least DATA_SLICES)";
+        case TE_ERR_BAD_ENCODING: return "invalid padding in recovered data";
+        case TE_ERR_INVALID_LAYOUT: return "invalid layout or inconsistent slices";
+        case TE_ERR_NOT_ENOUGH_HELPERS: return "not enough helpers";
+        case TE_ERR_INVALID_SLICE: return "invalid slice index";
+        case TE_ERR_CLAY: return "clay error";
+        case TE_ERR_MISSING_HELPER: return "missing helper data";
+        case TE_ERR_INVALID_ARG: return "invalid argument";
+        case TE_ERR_NO_DEVICE: return "no gfx950 HIP device available (libtapeec has no CPU fallback)";
+        case TE_ERR_HIP: return "HIP runtime error";
+        case TE_ERR_UNSUPPORTED: return "profile/layout not supported by the GPU engine";
+        case TE_ERR_OUT_OF_MEMORY: return "out of device memory";
+        case TE_ERR_BUFFER_TOO_SMALL: return "output buffer too small";
+    }
+    return "unknown status";
+}
+
+int te_device_count(void) { return device_count(); }
+
+int te_set_device(int device) {
+    if (device < 0 || device >= device_count()) return TE_ERR_NO_DEVICE;
+    TE_HIP(hipSetDevice(device));
+    return TE_OK;
+}
+
+const char *te_version(void) { return "tapeec 0.1.0 (gfx950)"; }
+
+// ------------------------------------------------------------------------------------------
+int te_clay_new(uint32_t n, uint32_t k, uint32_t d, te_clay **out) {
+    if (!out) return TE_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (n > TE_GROUP_SIZE) return TE_ERR_INVALID_ARG;
+    te_clay *c = new (std::nothrow) te_clay();
+    if (!c) return TE_ERR_OUT_OF_MEMORY;
+    const int r = c->h.init((int)n, (int)k, (int)d);
+    if (r) {
+        delete c;
+        return r == -1 ? TE_ERR_INVALID_ARG : TE_ERR_UNSUPPORTED;
+    }
+    c->fast_encode = encode_rows_supported((int)n, (int)k, (int)d);
+    *out = c;
+    return TE_OK;
+}
+
+int te_clay_from_params(uint64_t p, te_clay **out) {
+    return te_clay_new((uint32_t)(p & 0xFF), (uint32_t)((p >> 8) & 0xFF), (uint32_t)((p >> 16) & 0xFF), out);
+}
+
+void te_clay_free(te_clay *c) {
+    if (!c) return;
+    if (device_count() > 0) {
+        if (c->stream) (void)hipStreamSynchronize(c->stream);
+        c->enc.release();
+        c->dec.release();
+        c->rep.release();
+        c->io_in.release();
+        c->io_out.release();
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+    }
+    delete c;
+}
+
+int te_clay_get_info(const te_clay *c, te_clay_info *o) {
+    if (!c || !o) return TE_ERR_INVALID_ARG;
+    const ClayHost &h = c->h;
+    o->n = h.n; o->k = h.k; o->m = h.m; o->d = h.d;
+    o->q = h.q; o->t = h.t; o->nu = h.nu; o->alpha = h.alpha; o->beta = h.beta;
+    return TE_OK;
+}
+
+size_t te_clay_chunk_size_for(const te_clay *c, size_t len) { return c ? c->h.chunk_size_for(len) : 0; }
+
+size_t te_clay_track_chunk_size(const te_clay *c, size_t stripe, size_t blob_len) {
+    return c ? c->h.chunk_size_for(std::min(stripe, blob_len)) : 0;
+}
+
+// ------------------------------------------------------------------------------------------
+size_t te_pick_stripe_size(size_t blob_len) {
+    if (blob_len <= 1000000) return kStripeSizes[0];
+    if (blob_len <= 100000000) return kStripeSizes[1];
+    return kStripeSizes[2];
+}
+
+size_t te_num_stripes(size_t blob_len, size_t stripe) {
+    if (blob_len == 0) return 1;
+    if (stripe == 0) return 0;
+    return (blob_len + stripe - 1) / stripe;
+}
+
+uint32_t te_shard_to_slice(int rotated, uint32_t n, uint32_t stripe, uint32_t shard) {
+    if (!rotated || n == 0) return shard;
+    const uint32_t off = (uint32_t)(((uint64_t)stripe * TE_ROTATION_STEP) % n);
+    return (shard + off) % n;
+}
+
+uint32_t te_slice_to_shard(int rotated, uint32_t n, uint32_t stripe, uint32_t slice) {
+    if (!rotated || n == 0) return slice;
+    const uint32_t off = (uint32_t)(((uint64_t)stripe * TE_ROTATION_STEP) % n);
+    return (slice + n - off) % n;
+}
+
+void te_slice_metadata_to_bytes(const te_slice_metadata *m, uint8_t out[TE_META_SIZE]) {
+    put_u64(out, m->version);
+    put_u64(out + 8, m->blob_len);
+    put_u64(out + 16, m->stripe_size);
+    put_u64(out + 24, m->encoding);
+    put_u64(out + 32, m->params);
+    put_u64(out + 40, m->chunk_index);
+}
+
+int te_slice_metadata_from_slice(const uint8_t *slice, size_t len, te_slice_metadata *out) {
+    if (!slice || !out || len < TE_META_SIZE) return TE_ERR_INVALID_LAYOUT;
+    const uint8_t *p = slice + len - TE_META_SIZE;
+    out->version = get_u64(p);
+    out->blob_len = get_u64(p + 8);
+    out->stripe_size = get_u64(p + 16);
+    out->encoding = get_u64(p + 24);
+    out->params = get_u64(p + 32);
+    out->chunk_index = get_u64(p + 40);
+    if (!valid_stripe(out->stripe_size)) return TE_ERR_INVALID_LAYOUT;
+    return TE_OK;
+}
+
+int te_slicer_geometry(const te_clay *c, size_t blob_len, te_geometry *g) {
+    if (!c || !g) return TE_ERR_INVALID_ARG;
+    const size_t S = te_pick_stripe_size(blob_len);
+    const size_t ns = te_num_stripes(blob_len, S);
+    const size_t eff = blob_len == 0 ? S : std::min(blob_len, S);
+    const size_t cs = c->h.chunk_size_for(eff);
+    g->stripe_size = S;
+    g->num_stripes = ns;
+    g->chunk_size = cs;
+    g->sub_chunk_size = cs / (size_t)c->h.alpha;
+    g->slice_len = ns * cs + TE_META_SIZE;
+    return TE_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// Encode
+// ------------------------------------------------------------------------------------------
+namespace {
+
+struct GeomKey {
+    uint64_t cs, slice_len;
+    bool operator<(const GeomKey &o) const { return cs != o.cs ? cs < o.cs : slice_len < o.slice_len; }
+};
+
+int ensure_stream(te_clay *c) {
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    if (!c->stream) TE_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    return TE_OK;
+}
+
+// Enqueue the encode of a batch.  raw = ClayCoder::encode semantics (no slicing/rotation/meta,
+// slices are the n chunks of one padded input).
+int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, const te_object *objs,
+                   size_t nobj, uint8_t *d_out, hipStream_t s, bool raw) {
+    const ClayHost &h = c->h;
+    const int n = h.n;
+    const int rotated = cfg ? cfg->rotated : 0;
+    std::map<GeomKey, std::vector<EncJob>> groups;
+    std::vector<MetaJob> metas;
+    for (size_t i = 0; i < nobj; i++) {
+        const te_object &o = objs[i];
+        size_t S, ns, cs, slice_len;
+        if (raw) {
+            if (o.blob_len == 0) return TE_ERR_EMPTY_INPUT;
+            cs = h.chunk_size_for(o.blob_len);
+            S = cs * h.k;
+            ns = 1;
+            slice_len = cs;
+        } else {
+            te_geometry g;
+            te_slicer_geometry(c, o.blob_len, &g);
+            S = g.stripe_size; ns = g.num_stripes; cs = g.chunk_size; slice_len = g.slice_len;
+        }
+        if (cs % (size_t)h.alpha || slice_len > 0xffffffffull || cs > 0xffffffffull) return TE_ERR_TOO_MUCH_DATA;
+        auto &jobs = groups[GeomKey{cs, slice_len}];
+        for (size_t st = 0; st < ns; st++) {
+            EncJob j{};
+            const uint64_t start = (uint64_t)st * S;
+            j.src = d_data + o.data_off + start;
+            j.src_len = o.blob_len == 0 ? 0 : std::min<uint64_t>(S, o.blob_len - start);
+            j.dst = d_out + o.out_off + st * cs;
+            j.rot = rotated ? (uint32_t)((st * TE_ROTATION_STEP) % n) : 0u;
+            jobs.push_back(j);
+        }
+        if (!raw) {
+            MetaJob m{};
+            m.dst = d_out + o.out_off + ns * cs;
+            m.slice_len = slice_len;
+            m.words[0] = 0;
+            m.words[1] = o.blob_len;
+            m.words[2] = S;
+            m.words[3] = cfg ? cfg->encoding : TE_ENCODING_CLAY;
+            m.words[4] = cfg ? cfg->params : TE_CLAY_DEFAULT_PARAMS;
+            m.words[5] = o.chunk_index;
+            metas.push_back(m);
+        }
+    }
+    // descriptor image
+    Arena &A = c->enc;
+    A.img.clear();
+    struct Launch { GeomKey key; size_t off, count; };
+    std::vector<Launch> launches;
+    for (auto &kv : groups) launches.push_back({kv.first, A.put(kv.second.data(), kv.second.size() * sizeof(EncJob)), kv.second.size()});
+    const size_t meta_off = A.put(metas.data(), metas.size() * sizeof(MetaJob));
+    // generic-engine pattern (parity erased) for profiles outside the fast path
+    size_t pat_off = 0, pool_off = 0;
+    GpePattern pat{};
+    std::vector<uint16_t> pool;
+    std::vector<GpeJob> gjobs;
+    std::vector<size_t> gjob_off;
+    if (!c->fast_encode) {
+        uint64_t mask = 0;
+        for (int i = h.k + h.nu; i < h.qt; i++) mask |= 1ull << i;
+        if (!h.gpe_pattern(mask, pat, pool)) return TE_ERR_UNSUPPORTED;
+        pat_off = A.put(&pat, sizeof(pat));
+        pool_off = A.put(pool.data(), pool.size() * sizeof(uint16_t));
+        for (auto &kv : groups) {
+            std::vector<GpeJob> gj;
+            for (const EncJob &e : kv.second) {
+                GpeJob g{};
+                g.in = e.src; g.out = e.dst; g.in_len = e.src_len; g.out_len = ~0ull; g.rot = e.rot; g.pattern = 0;
+                gj.push_back(g);
+            }
+            gjob_off.push_back(A.put(gj.data(), gj.size() * sizeof(GpeJob)));
+        }
+    }
+    int r = A.upload(s);
+    if (r) return r;
+    if (!metas.empty()) TE_HIP(launch_meta(A.at<MetaJob>(meta_off), (uint32_t)metas.size(), (uint32_t)n, s));
+    size_t gi = 0;
+    for (const Launch &L : launches) {
+        const uint32_t cs = (uint32_t)L.key.cs, sc = cs / (uint32_t)h.alpha;
+        const uint32_t wps = sc >= 4 ? (sc + 3) / 4 : 1;
+        if (c->fast_encode) {
+            EncArgs a{};
+            a.jobs = A.at<EncJob>(L.off);
+            a.total_words = (uint64_t)L.count * wps;
+            a.words_per_stripe = wps;
+            a.cs = cs;
+            a.sc = sc;
+            a.slice_len = (uint32_t)L.key.slice_len;
+            a.n = (uint32_t)n;
+            TE_HIP(launch_encode_rows(h.k, a, s));
+        } else {
+            GpeArgs a{};
+            a.jobs = A.at<GpeJob>(gjob_off[gi]);
+            a.patterns = A.at<GpePattern>(pat_off);
+            a.plane_pool = A.at<uint16_t>(pool_off);
+            a.njobs = (uint32_t)L.count;
+            a.words_per_stripe = wps;
+            a.groups_per_stripe = (wps + kGpeWords - 1) / kGpeWords;
+            a.cs = cs; a.sc = sc; a.q = h.q; a.t = h.t; a.k = h.k; a.nu = h.nu; a.n = n; a.alpha = h.alpha;
+            a.in_stride = cs; a.out_stride = L.key.slice_len;
+            a.in_rotated = 0; a.out_rotated = 1;
+            a.out_mask = 0;
+            for (int i = 0; i < h.qt; i++)
+                if (h.int_to_ext(i) >= 0) a.out_mask |= 1ull << i;
+            for (int i = 0; i < 16; i++) a.qpow[i] = h.qpow[i];
+            TE_HIP(launch_gpe(a, (uint32_t)pat.nerased, s));
+        }
+        gi++;
+    }
+    return A.mark_done(s);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// Decode
+// ------------------------------------------------------------------------------------------
+namespace {
+
+struct DecItem {          // one object, host-validated
+    uint64_t in_base;     // offset in d_slices of slice 0
+    uint64_t slice_len, blob_len, stripe, ns, cs, out_off;
+    uint32_t avail;
+};
+
+// Validate one object like Slicer::decode (slicer.rs:298-331, validate_layout :79-105).
+int decode_validate(const te_clay *c, const uint8_t *meta48, uint64_t slice_len, uint32_t avail, DecItem &it) {
+    const ClayHost &h = c->h;
+    const int na = __builtin_popcount(avail & ((h.n >= 32) ? 0xffffffffu : ((1u << h.n) - 1u)));
+    if (na == 0) return TE_ERR_NOT_ENOUGH_SLICES;
+    te_slice_metadata m;
+    int r = te_slice_metadata_from_slice(meta48, TE_META_SIZE, &m);
+    if (r) return r;
+    const uint32_t pk = (uint32_t)((m.params >> 8) & 0xFF);  // profile k  slicer.rs:308-311
+    if ((uint32_t)na < pk) return TE_ERR_NOT_ENOUGH_SLICES;
+    it.blob_len = m.blob_len;
+    it.stripe = m.stripe_size;
+    it.slice_len = slice_len;
+    it.avail = avail;
+    if (m.blob_len == 0) { it.ns = 0; it.cs = 0; return TE_OK; }
+    it.ns = (m.blob_len + m.stripe_size - 1) / m.stripe_size;
+    const uint64_t total = slice_len >= TE_META_SIZE ? slice_len - TE_META_SIZE : 0;
+    if (total == 0 || total % it.ns) return TE_ERR_INVALID_LAYOUT;
+    it.cs = total / it.ns;
+    if (na < h.k) return TE_ERR_NOT_ENOUGH_SLICES;  // ClayCoder::decode clay.rs:107-109
+    if (it.cs % (uint64_t)h.alpha) return TE_ERR_BAD_ENCODING;
+    // take <= decoded stripe size (slicer.rs:351-357)
+    const uint64_t last_take = m.blob_len - (it.ns - 1) * m.stripe_size;
+    if (std::max<uint64_t>(it.ns > 1 ? m.stripe_size : 0, last_take) > it.cs * (uint64_t)h.k) return TE_ERR_INVALID_LAYOUT;
+    return TE_OK;
+}
+
+int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices, const DecItem *items,
+                   size_t nitems, uint8_t *d_out, hipStream_t s, bool raw) {
+    const ClayHost &h = c->h;
+    const int n = h.n;
+    const int rotated = (cfg && !raw) ? cfg->rotated : 0;
+    std::map<uint64_t, uint32_t> pat_index;  // erased mask -> pattern id
+    std::vector<GpePattern> pats;
+    std::vector<uint16_t> pool;
+    std::map<uint64_t, std::vector<GpeJob>> groups;  // by chunk size
+    std::map<uint64_t, uint64_t> group_in_stride;
+    uint32_t max_er = 0;
+    for (size_t i = 0; i < nitems; i++) {
+        const DecItem &it = items[i];
+        for (uint64_t st = 0; st < it.ns; st++) {
+            uint64_t emask = 0;
+            for (int sh = 0; sh < n; sh++) {
+                const uint32_t sl = te_shard_to_slice(rotated, (uint32_t)n, (uint32_t)st, (uint32_t)sh);
+                if (!((it.avail >> sl) & 1u)) emask |= 1ull << h.ext_to_int(sh);
+            }
+            emask = h.pad_erasures(emask);
+            auto f = pat_index.find(emask);
+            uint32_t pid;
+            if (f == pat_index.end()) {
+                GpePattern P;
+                if (!h.gpe_pattern(emask, P, pool)) return TE_ERR_BAD_ENCODING;
+                pid = (uint32_t)pats.size();
+                pats.push_back(P);
+                pat_index[emask] = pid;
+                max_er = std::max(max_er, P.nerased);
+            } else {
+                pid = f->second;
+            }
+            GpeJob g{};
+            g.in = d_slices + it.in_base + st * it.cs;
+            g.out = d_out + it.out_off + st * (raw ? 0 : it.stripe);
+            g.in_len = ~0ull;
+            g.out_len = raw ? it.cs * (uint64_t)h.k : (st + 1 == it.ns ? it.blob_len - st * it.stripe : it.stripe);
+            g.rot = rotated ? (uint32_t)((st * TE_ROTATION_STEP) % n) : 0u;
+            g.pattern = pid;
+            auto key = (it.cs << 32) ^ it.slice_len;
+            groups[key].push_back(g);
+            group_in_stride[key] = it.slice_len;
+        }
+    }
+    if (groups.empty()) return TE_OK;
+    Arena &A = c->dec;
+    A.img.clear();
+    const size_t pat_off = A.put(pats.data(), pats.size() * sizeof(GpePattern));
+    const size_t pool_off = A.put(pool.data(), pool.size() * sizeof(uint16_t));
+    std::vector<std::pair<uint64_t, size_t>> offs;
+    for (auto &kv : groups) offs.push_back({kv.first, A.put(kv.second.data(), kv.second.size() * sizeof(GpeJob))});
+    int r = A.upload(s);
+    if (r) return r;
+    for (auto &o : offs) {
+        const uint64_t cs = o.first >> 32;
+        const uint32_t sc = (uint32_t)(cs / (uint64_t)h.alpha);
+        const uint32_t wps = sc >= 4 ? (sc + 3) / 4 : 1;
+        GpeArgs a{};
+        a.jobs = A.at<GpeJob>(o.second);
+        a.patterns = A.at<GpePattern>(pat_off);
+        a.plane_pool = A.at<uint16_t>(pool_off);
+        a.njobs = (uint32_t)groups[o.first].size();
+        a.words_per_stripe = wps;
+        a.groups_per_stripe = (wps + kGpeWords - 1) / kGpeWords;
+        a.cs = (uint32_t)cs; a.sc = sc; a.q = h.q; a.t = h.t; a.k = h.k; a.nu = h.nu; a.n = n; a.alpha = h.alpha;
+        a.in_stride = group_in_stride[o.first];
+        a.out_stride = cs;
+        a.in_rotated = rotated ? 1u : 0u;
+        a.out_rotated = 0;
+        a.out_mask = (h.k >= 64) ? ~0ull : ((1ull << h.k) - 1ull);
+        for (int i = 0; i < 16; i++) a.qpow[i] = h.qpow[i];
+        TE_HIP(launch_gpe(a, max_er, s));
+    }
+    return A.mark_done(s);
+}
+
+// ------------------------------------------------------------------------------------------
+// Repair
+// ------------------------------------------------------------------------------------------
+struct RepItem {
+    const te_repair_plan *plan;
+    const uint64_t *helper_off;  // [n] offsets into d_helpers by slice id (UINT64_MAX = absent)
+    uint64_t out_off;
+    const uint8_t *meta;         // 48 bytes or null (raw)
+};
+
+int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, size_t nitems, uint8_t *d_out,
+                   hipStream_t s) {
+    const ClayHost &h = c->h;
+    std::map<std::vector<int>, uint32_t> pat_index;  // (lost, helpers...) -> pattern id
+    std::vector<RepPattern> pats;
+    std::vector<uint16_t> pool, pind;
+    std::map<uint64_t, std::vector<RepJob>> groups;  // by chunk size
+    std::vector<MetaJob> metas;
+    uint32_t max_er = 0;
+    for (size_t i = 0; i < nitems; i++) {
+        const te_repair_plan *p = items[i].plan;
+        std::vector<uint64_t> run(p->n, 0);
+        for (uint32_t st = 0; st < p->ns; st++) {
+            std::vector<int> key;
+            key.push_back((int)p->lost_shard[st]);
+            std::vector<int> hs;
+            for (uint32_t j = 0; j < p->d; j++) hs.push_back((int)p->helper_shard[st * p->d + j]);
+            key.insert(key.end(), hs.begin(), hs.end());
+            auto f = pat_index.find(key);
+            uint32_t pid;
+            if (f == pat_index.end()) {
+                RepPattern P;
+                if (!h.rep_pattern((int)p->lost_shard[st], hs, P, pool, pind)) return TE_ERR_CLAY;
+                pid = (uint32_t)pats.size();
+                pats.push_back(P);
+                pat_index[key] = pid;
+                max_er = std::max(max_er, P.nerased);
+            } else {
+                pid = f->second;
+            }
+            RepJob j{};
+            for (uint32_t hj = 0; hj < p->d; hj++) {
+                const uint32_t sl = p->helper_slice[st * p->d + hj];
+                const uint32_t sh = p->helper_shard[st * p->d + hj];
+                const uint64_t off = items[i].helper_off[sl];
+                if (off == ~0ull) return TE_ERR_MISSING_HELPER;
+                j.helper[h.ext_to_int((int)sh)] = d_helpers + off + run[sl];
+                run[sl] += (uint64_t)p->beta * p->sc;
+            }
+            j.out = d_out + items[i].out_off + (uint64_t)st * p->cs;
+            j.pattern = pid;
+            groups[p->cs].push_back(j);
+        }
+        if (items[i].meta) {
+            MetaJob m{};
+            m.dst = d_out + items[i].out_off + (uint64_t)p->ns * p->cs;
+            m.slice_len = 0;
+            for (int w = 0; w < 6; w++) m.words[w] = get_u64(items[i].meta + 8 * w);
+            metas.push_back(m);
+        }
+    }
+    Arena &A = c->rep;
+    A.img.clear();
+    const size_t pat_off = A.put(pats.data(), pats.size() * sizeof(RepPattern));
+    const size_t pool_off = A.put(pool.data(), pool.size() * sizeof(uint16_t));
+    const size_t pind_off = A.put(pind.data(), pind.size() * sizeof(uint16_t));
+    const size_t meta_off = A.put(metas.data(), metas.size() * sizeof(MetaJob));
+    std::vector<std::pair<uint64_t, size_t>> offs;
+    for (auto &kv : groups) offs.push_back({kv.first, A.put(kv.second.data(), kv.second.size() * sizeof(RepJob))});
+    int r = A.upload(s);
+    if (r) return r;
+    if (!metas.empty()) TE_HIP(launch_meta(A.at<MetaJob>(meta_off), (uint32_t)metas.size(), 1u, s));
+    for (auto &o : offs) {
+        const uint64_t cs = o.first;
+        const uint32_t sc = (uint32_t)(cs / (uint64_t)h.alpha);
+        const uint32_t wps = sc >= 4 ? (sc + 3) / 4 : 1;
+        RepArgs a{};
+        a.jobs = A.at<RepJob>(o.second);
+        a.patterns = A.at<RepPattern>(pat_off);
+        a.plane_pool = A.at<uint16_t>(pool_off);
+        a.plane_ind = A.at<uint16_t>(pind_off);
+        a.njobs = (uint32_t)groups[o.first].size();
+        a.words_per_stripe = wps;
+        a.groups_per_stripe = (wps + kGpeWords - 1) / kGpeWords;
+        a.cs = (uint32_t)cs; a.sc = sc; a.q = h.q; a.t = h.t; a.alpha = h.alpha;
+        for (int i = 0; i < 16; i++) a.qpow[i] = h.qpow[i];
+        TE_HIP(launch_repair(a, max_er, s));
+    }
+    return A.mark_done(s);
+}
+
+int build_plan(const te_clay *c, int rotated, uint32_t lost, const uint32_t *avail, size_t navail, uint64_t ns,
+               uint64_t cs, te_repair_plan **out) {
+    const ClayHost &h = c->h;
+    if (lost >= (uint32_t)h.n) return TE_ERR_INVALID_SLICE;
+    if (cs % (uint64_t)h.alpha) return TE_ERR_INVALID_LAYOUT;
+    te_repair_plan *p = new (std::nothrow) te_repair_plan();
+    if (!p) return TE_ERR_OUT_OF_MEMORY;
+    p->lost = lost; p->ns = (uint32_t)ns; p->d = (uint32_t)h.d; p->beta = (uint32_t)h.beta; p->n = (uint32_t)h.n;
+    p->cs = cs; p->sc = cs / (uint64_t)h.alpha;
+    for (uint64_t st = 0; st < ns; st++) {
+        const int ls = (int)te_slice_to_shard(rotated, (uint32_t)h.n, (uint32_t)st, lost);
+        std::vector<int> av;
+        for (size_t i = 0; i < navail; i++) {
+            if (avail[i] >= (uint32_t)h.n) { delete p; return TE_ERR_INVALID_SLICE; }
+            av.push_back((int)te_slice_to_shard(rotated, (uint32_t)h.n, (uint32_t)st, avail[i]));
+        }
+        std::vector<int> hs;
+        const int r = h.min_to_repair(ls, av, hs);
+        if (r) { delete p; return r == -1 ? TE_ERR_NOT_ENOUGH_HELPERS : TE_ERR_CLAY; }
+        const std::vector<int> planes = h.repair_planes(ls);
+        p->lost_shard.push_back((uint32_t)ls);
+        for (int sh : hs) {
+            p->helper_shard.push_back((uint32_t)sh);
+            p->helper_slice.push_back(te_shard_to_slice(rotated, (uint32_t)h.n, (uint32_t)st, (uint32_t)sh));
+            for (int z : planes) p->sub_chunks.push_back((uint32_t)z);
+        }
+    }
+    *out = p;
+    return TE_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// C ABI: compute entry points
+// ------------------------------------------------------------------------------------------
+extern "C" {
+
+int te_encode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, const te_object *objs,
+                           size_t nobj, uint8_t *d_out, void *stream) {
+    if (!c || !cfg || (!objs && nobj)) return TE_ERR_INVALID_ARG;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    std::lock_guard<std::mutex> lk(c->mu);
+    return encode_enqueue(c, cfg, d_data, objs, nobj, d_out, (hipStream_t)stream, false);
+}
+
+int te_decode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices, const te_decode_object *objs,
+                           const uint8_t *h_meta, size_t nobj, uint8_t *d_out, void *stream) {
+    if (!c || !cfg || (!objs && nobj) || (!h_meta && nobj)) return TE_ERR_INVALID_ARG;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    std::vector<DecItem> items(nobj);
+    for (size_t i = 0; i < nobj; i++) {
+        int r = decode_validate(c, h_meta + i * TE_META_SIZE, objs[i].slice_len, objs[i].avail_mask, items[i]);
+        if (r) return r;
+        items[i].in_base = objs[i].slices_off;
+        items[i].out_off = objs[i].out_off;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    return decode_enqueue(c, cfg, d_slices, items.data(), items.size(), d_out, (hipStream_t)stream, false);
+}
+
+int te_repair_batch_device(te_clay *c, const uint8_t *d_helpers, const te_repair_object *objs, size_t nobj,
+                           uint8_t *d_out, void *stream) {
+    if (!c || (!objs && nobj)) return TE_ERR_INVALID_ARG;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    std::vector<RepItem> items(nobj);
+    for (size_t i = 0; i < nobj; i++) {
+        if (!objs[i].plan) return TE_ERR_INVALID_ARG;
+        if (objs[i].plan->n != (uint32_t)c->h.n || objs[i].plan->d != (uint32_t)c->h.d) return TE_ERR_INVALID_ARG;
+        items[i] = RepItem{objs[i].plan, objs[i].helper_off, objs[i].out_off, objs[i].metadata};
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    return repair_enqueue(c, d_helpers, items.data(), items.size(), d_out, (hipStream_t)stream);
+}
+
+int te_slicer_encode(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *data, size_t len, uint8_t *slices,
+                     size_t cap) {
+    if (!c || !cfg || (!data && len) || !slices) return TE_ERR_INVALID_ARG;
+    te_geometry g;
+    te_slicer_geometry(c, len, &g);
+    const size_t total = (size_t)c->h.n * g.slice_len;
+    if (cap < total) return TE_ERR_BUFFER_TOO_SMALL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    int r = ensure_stream(c);
+    if (r) return r;
+    TE_HIP(c->io_in.ensure(len + 16));
+    TE_HIP(c->io_out.ensure(total));
+    if (len) TE_HIP(hipMemcpyAsync(c->io_in.p, data, len, hipMemcpyHostToDevice, c->stream));
+    te_object o{0, len, 0, cfg->chunk_index};
+    r = encode_enqueue(c, cfg, c->io_in.as<uint8_t>(), &o, 1, c->io_out.as<uint8_t>(), c->stream, false);
+    if (r) return r;
+    TE_HIP(hipMemcpyAsync(slices, c->io_out.p, total, hipMemcpyDeviceToHost, c->stream));
+    TE_HIP(hipStreamSynchronize(c->stream));
+    return TE_OK;
+}
+
+int te_clay_encode(te_clay *c, const uint8_t *data, size_t len, uint8_t *chunks, size_t cap, size_t *chunk_size) {
+    if (!c || (!data && len) || !chunks) return TE_ERR_INVALID_ARG;
+    if (len == 0) return TE_ERR_EMPTY_INPUT;  // clay.rs:100-102
+    const size_t cs = c->h.chunk_size_for(len);
+    const size_t total = (size_t)c->h.n * cs;
+    if (chunk_size) *chunk_size = cs;
+    if (cap < total) return TE_ERR_BUFFER_TOO_SMALL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    int r = ensure_stream(c);
+    if (r) return r;
+    TE_HIP(c->io_in.ensure(len + 16));
+    TE_HIP(c->io_out.ensure(total));
+    TE_HIP(hipMemcpyAsync(c->io_in.p, data, len, hipMemcpyHostToDevice, c->stream));
+    te_object o{0, len, 0, 0};
+    te_slicer_cfg cfg{0, TE_ENCODING_CLAY, TE_CLAY_DEFAULT_PARAMS, 0};
+    r = encode_enqueue(c, &cfg, c->io_in.as<uint8_t>(), &o, 1, c->io_out.as<uint8_t>(), c->stream, true);
+    if (r) return r;
+    TE_HIP(hipMemcpyAsync(chunks, c->io_out.p, total, hipMemcpyDeviceToHost, c->stream));
+    TE_HIP(hipStreamSynchronize(c->stream));
+    return TE_OK;
+}
+
+int te_clay_decode(te_clay *c, const uint8_t *const *chunks, size_t cs, uint8_t *out, size_t cap) {
+    if (!c || !chunks || !out) return TE_ERR_INVALID_ARG;
+    const ClayHost &h = c->h;
+    uint32_t avail = 0;
+    int na = 0;
+    for (int i = 0; i < h.n; i++)
+        if (chunks[i]) { avail |= 1u << i; na++; }
+    if (na < h.k) return TE_ERR_NOT_ENOUGH_SLICES;  // clay.rs:107-109
+    if (cs == 0 || cs % (size_t)h.alpha) return TE_ERR_BAD_ENCODING;
+    if (cap < (size_t)h.k * cs) return TE_ERR_BUFFER_TOO_SMALL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    int r = ensure_stream(c);
+    if (r) return r;
+    const size_t total = (size_t)h.n * cs;
+    TE_HIP(c->io_in.ensure(total));
+    TE_HIP(c->io_out.ensure((size_t)h.k * cs));
+    for (int i = 0; i < h.n; i++)
+        if (chunks[i])
+            TE_HIP(hipMemcpyAsync(c->io_in.as<uint8_t>() + (size_t)i * cs, chunks[i], cs, hipMemcpyHostToDevice, c->stream));
+    DecItem it{};
+    it.in_base = 0; it.slice_len = cs; it.blob_len = (uint64_t)h.k * cs; it.stripe = it.blob_len; it.ns = 1; it.cs = cs;
+    it.out_off = 0; it.avail = avail;
+    r = decode_enqueue(c, nullptr, c->io_in.as<uint8_t>(), &it, 1, c->io_out.as<uint8_t>(), c->stream, true);
+    if (r) return r;
+    TE_HIP(hipMemcpyAsync(out, c->io_out.p, (size_t)h.k * cs, hipMemcpyDeviceToHost, c->stream));
+    TE_HIP(hipStreamSynchronize(c->stream));
+    return TE_OK;
+}
+
+int te_slicer_decode(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *const *slices, size_t slice_len,
+                     uint8_t *out, size_t cap, size_t *out_len) {
+    if (!c || !cfg || !slices) return TE_ERR_INVALID_ARG;
+    const ClayHost &h = c->h;
+    uint32_t avail = 0;
+    int first = -1;
+    for (int i = 0; i < h.n; i++)
+        if (slices[i]) { avail |= 1u << i; if (first < 0) first = i; }
+    if (first < 0) return TE_ERR_NOT_ENOUGH_SLICES;
+    if (slice_len < TE_META_SIZE) return TE_ERR_INVALID_LAYOUT;
+    DecItem it{};
+    int r = decode_validate(c, slices[first] + slice_len - TE_META_SIZE, slice_len, avail, it);
+    if (r) return r;
+    if (out_len) *out_len = it.blob_len;
+    if (it.blob_len == 0) return TE_OK;
+    if (!out || cap < it.blob_len) return TE_ERR_BUFFER_TOO_SMALL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    r = ensure_stream(c);
+    if (r) return r;
+    const size_t total = (size_t)h.n * slice_len;
+    TE_HIP(c->io_in.ensure(total));
+    TE_HIP(c->io_out.ensure(it.blob_len));
+    for (int i = 0; i < h.n; i++)
+        if (slices[i])
+            TE_HIP(hipMemcpyAsync(c->io_in.as<uint8_t>() + (size_t)i * slice_len, slices[i], slice_len,
+                                  hipMemcpyHostToDevice, c->stream));
+    it.in_base = 0;
+    it.out_off = 0;
+    r = decode_enqueue(c, cfg, c->io_in.as<uint8_t>(), &it, 1, c->io_out.as<uint8_t>(), c->stream, false);
+    if (r) return r;
+    TE_HIP(hipMemcpyAsync(out, c->io_out.p, it.blob_len, hipMemcpyDeviceToHost, c->stream));
+    TE_HIP(hipStreamSynchronize(c->stream));
+    return TE_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Repair planning (host only)
+// ------------------------------------------------------------------------------------------
+int te_clay_plan_repair(const te_clay *c, uint32_t lost, const uint32_t *available, size_t navail,
+                        uint32_t *helpers_out, uint32_t *sub_chunks_out) {
+    if (!c || (!available && navail)) return TE_ERR_INVALID_ARG;
+    const ClayHost &h = c->h;
+    if (lost >= (uint32_t)h.n) return TE_ERR_INVALID_SLICE;
+    std::vector<int> av(available, available + navail), hs;
+    const int r = h.min_to_repair((int)lost, av, hs);
+    if (r) return r == -1 ? TE_ERR_NOT_ENOUGH_HELPERS : TE_ERR_CLAY;
+    if (helpers_out)
+        for (size_t i = 0; i < hs.size(); i++) helpers_out[i] = (uint32_t)hs[i];
+    if (sub_chunks_out) {
+        const std::vector<int> pl = h.repair_planes((int)lost);
+        for (size_t i = 0; i < pl.size(); i++) sub_chunks_out[i] = (uint32_t)pl[i];
+    }
+    return TE_OK;
+}
+
+int te_repair_plan_from_params(const te_clay *c, int rotated, uint32_t lost, const uint32_t *avail, size_t navail,
+                               uint64_t blob_len, uint64_t stripe, te_repair_plan **out) {
+    if (!c || !out || (!avail && navail) || stripe == 0) return TE_ERR_INVALID_ARG;
+    *out = nullptr;
+    const uint64_t ns = blob_len == 0 ? 1 : (blob_len + stripe - 1) / stripe;
+    const uint64_t cs = c->h.chunk_size_for(std::min(stripe, blob_len));  // track_chunk_size
+    return build_plan(c, rotated, lost, avail, navail, ns, cs, out);
+}
+
+int te_repair_plan_from_slice(const te_clay *c, int rotated, uint32_t lost, const uint32_t *avail, size_t navail,
+                              const uint8_t *ref, size_t ref_len, te_repair_plan **out) {
+    if (!c || !out || !ref) return TE_ERR_INVALID_ARG;
+    *out = nullptr;
+    te_slice_metadata m;
+    if (te_slice_metadata_from_slice(ref, ref_len, &m)) return TE_ERR_INVALID_LAYOUT;
+    const uint64_t ns = m.blob_len == 0 ? 1 : (m.blob_len + m.stripe_size - 1) / m.stripe_size;
+    const uint64_t total = ref_len >= TE_META_SIZE ? ref_len - TE_META_SIZE : 0;
+    if (total == 0 || total % ns) return TE_ERR_INVALID_LAYOUT;
+    return build_plan(c, rotated, lost, avail, navail, ns, total / ns, out);
+}
+
+void te_repair_plan_free(te_repair_plan *p) { delete p; }
+
+int te_repair_plan_get_info(const te_repair_plan *p, te_repair_plan_info *o) {
+    if (!p || !o) return TE_ERR_INVALID_ARG;
+    o->lost = p->lost; o->num_stripes = p->ns; o->d = p->d; o->beta = p->beta;
+    o->chunk_size = p->cs; o->sub_chunk_size = p->sc;
+    return TE_OK;
+}
+
+int te_repair_plan_stripe(const te_repair_plan *p, uint32_t st, uint32_t *lost_shard, uint32_t *helper_slices,
+                          uint32_t *helper_shards, uint32_t *sub_chunks) {
+    if (!p || st >= p->ns) return TE_ERR_INVALID_ARG;
+    if (lost_shard) *lost_shard = p->lost_shard[st];
+    for (uint32_t j = 0; j < p->d; j++) {
+        if (helper_slices) helper_slices[j] = p->helper_slice[st * p->d + j];
+        if (helper_shards) helper_shards[j] = p->helper_shard[st * p->d + j];
+        if (sub_chunks)
+            for (uint32_t b = 0; b < p->beta; b++) sub_chunks[j * p->beta + b] = p->sub_chunks[(st * p->d + j) * p->beta + b];
+    }
+    return TE_OK;
+}
+
+size_t te_extract_repair_data_size(const te_repair_plan *p, uint32_t helper) {
+    if (!p) return 0;
+    size_t total = 0;
+    for (uint32_t st = 0; st < p->ns; st++)
+        for (uint32_t j = 0; j < p->d; j++)
+            if (p->helper_slice[st * p->d + j] == helper) total += (size_t)p->beta * p->sc;
+    return total;
+}
+
+int te_extract_repair_data(const te_repair_plan *p, const uint8_t *slice, size_t slice_len, uint32_t helper,
+                           uint8_t *out, size_t cap, size_t *out_len) {
+    if (!p || !slice) return TE_ERR_INVALID_ARG;
+    const size_t need = te_extract_repair_data_size(p, helper);
+    if (out_len) *out_len = need;
+    if (cap < need || (!out && need)) return TE_ERR_BUFFER_TOO_SMALL;
+    size_t w = 0;
+    for (uint32_t st = 0; st < p->ns; st++) {
+        const uint64_t co = (uint64_t)st * p->cs;
+        for (uint32_t j = 0; j < p->d; j++) {
+            if (p->helper_slice[st * p->d + j] != helper) continue;
+            if (co + p->cs > slice_len) return TE_ERR_INVALID_LAYOUT;  // "slice too short for chunk"
+            for (uint32_t b = 0; b < p->beta; b++) {
+                const uint64_t z = p->sub_chunks[(st * p->d + j) * p->beta + b];
+                if ((z + 1) * p->sc > p->cs) return TE_ERR_INVALID_LAYOUT;  // "sub-chunk out of bounds"
+                memcpy(out + w, slice + co + z * p->sc, p->sc);
+                w += p->sc;
+            }
+        }
+    }
+    return TE_OK;
+}
+
+int te_slicer_repair(te_clay *c, const te_repair_plan *p, const uint8_t *const *helper_data, const size_t *helper_lens,
+                     const uint8_t metadata[TE_META_SIZE], uint8_t *out, size_t cap) {
+    if (!c || !p || !helper_data || !helper_lens || !metadata || !out) return TE_ERR_INVALID_ARG;
+    if (p->n != (uint32_t)c->h.n || p->d != (uint32_t)c->h.d) return TE_ERR_INVALID_ARG;
+    const size_t out_bytes = (size_t)p->ns * p->cs + TE_META_SIZE;
+    if (cap < out_bytes) return TE_ERR_BUFFER_TOO_SMALL;
+    // per-helper byte need (Slicer::repair walks a running offset per helper: repair.rs:340-354)
+    std::vector<uint64_t> need(p->n, 0), off(p->n, ~0ull);
+    for (uint32_t st = 0; st < p->ns; st++)
+        for (uint32_t j = 0; j < p->d; j++) need[p->helper_slice[st * p->d + j]] += (uint64_t)p->beta * p->sc;
+    uint64_t total = 0;
+    for (uint32_t sl = 0; sl < p->n; sl++) {
+        if (!need[sl]) continue;
+        if (!helper_data[sl] || helper_lens[sl] < need[sl]) return TE_ERR_MISSING_HELPER;
+        off[sl] = total;
+        total += (need[sl] + 15) & ~15ull;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    int r = ensure_stream(c);
+    if (r) return r;
+    TE_HIP(c->io_in.ensure(total + 16));
+    TE_HIP(c->io_out.ensure(out_bytes));
+    for (uint32_t sl = 0; sl < p->n; sl++)
+        if (need[sl])
+            TE_HIP(hipMemcpyAsync(c->io_in.as<uint8_t>() + off[sl], helper_data[sl], need[sl], hipMemcpyHostToDevice,
+                                  c->stream));
+    RepItem it{p, off.data(), 0, metadata};
+    r = repair_enqueue(c, c->io_in.as<uint8_t>(), &it, 1, c->io_out.as<uint8_t>(), c->stream);
+    if (r) return r;
+    TE_HIP(hipMemcpyAsync(out, c->io_out.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
+    TE_HIP(hipStreamSynchronize(c->stream));
+    return TE_OK;
+}
+
+int te_clay_repair(te_clay *c, uint32_t lost, const uint32_t *helpers, const uint8_t *const *helper_data,
+                   size_t nhelpers, size_t chunk_size, uint8_t *out) {
+    if (!c || !helpers || !helper_data || !out) return TE_ERR_INVALID_ARG;
+    const ClayHost &h = c->h;
+    if (lost >= (uint32_t)h.n) return TE_ERR_INVALID_SLICE;
+    if (nhelpers != (size_t)h.d) return TE_ERR_NOT_ENOUGH_HELPERS;
+    if (chunk_size == 0 || chunk_size % (size_t)h.alpha) return TE_ERR_INVALID_LAYOUT;
+    // one-stripe, identity-mapped plan with the caller's helper set
+    te_repair_plan p;
+    p.lost = lost; p.ns = 1; p.d = (uint32_t)h.d; p.beta = (uint32_t)h.beta; p.n = (uint32_t)h.n;
+    p.cs = chunk_size; p.sc = chunk_size / (size_t)h.alpha;
+    p.lost_shard.push_back(lost);
+    const std::vector<int> planes = h.repair_planes((int)lost);
+    std::vector<const uint8_t *> by_slice(h.n, nullptr);
+    std::vector<size_t> lens(h.n, 0);
+    std::vector<int> hs;
+    for (size_t j = 0; j < nhelpers; j++) {
+        if (helpers[j] >= (uint32_t)h.n || helpers[j] == lost) return TE_ERR_INVALID_SLICE;
+        hs.push_back((int)helpers[j]);
+    }
+    std::sort(hs.begin(), hs.end());
+    for (size_t j = 0; j < nhelpers; j++) {
+        by_slice[helpers[j]] = helper_data[j];
+        lens[helpers[j]] = (size_t)h.beta * p.sc;
+    }
+    for (int sh : hs) {
+        p.helper_shard.push_back((uint32_t)sh);
+        p.helper_slice.push_back((uint32_t)sh);
+        for (int z : planes) p.sub_chunks.push_back((uint32_t)z);
+    }
+    std::vector<uint8_t> tmp(chunk_size + TE_META_SIZE);
+    uint8_t meta[TE_META_SIZE] = {0};
+    int r = te_slicer_repair(c, &p, by_slice.data(), lens.data(), meta, tmp.data(), tmp.size());
+    if (r) return r;
+    memcpy(out, tmp.data(), chunk_size);
+    return TE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,115 @@
+// kernels.hpp -- device job descriptors and launcher declarations shared by host and HIP code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "gf.hpp"
+
+namespace tec {
+
+// One stripe of one object for the encode kernels (Slicer::encode, slicer.rs:237-296).
+struct EncJob {
+    const uint8_t *src;   // first byte of the stripe in the object
+    uint8_t *dst;         // object's slice-0 base + stripe*chunk_size
+    uint64_t src_len;     // valid bytes of the stripe (rest is zero padding)
+    uint32_t rot;         // rotation offset (stripe*7) % n, 0 for identity mapping
+    uint32_t pad_;
+};
+
+struct EncArgs {
+    const EncJob *jobs;
+    uint64_t total_words;  // njobs * words_per_stripe
+    uint32_t words_per_stripe;
+    uint32_t cs;           // chunk size
+    uint32_t sc;           // sub-chunk size
+    uint32_t slice_len;
+    uint32_t n;
+};
+
+// Metadata suffix writer: one 48-byte record per object, copied to its n slices.
+struct MetaJob {
+    uint8_t *dst;          // object's slice-0 base + num_stripes*chunk_size
+    uint64_t slice_len;    // stride between the object's slices
+    uint64_t words[6];
+};
+
+// ---- generic layered engine (decode / generic encode) ----
+constexpr int kGpeMaxErased = 20;
+constexpr int kGpeMaxKnown = 20;
+
+// Erasure pattern of one stripe: which internal nodes are erased, the per-plane MDS decoder
+// (as v_perm tables) and the planes grouped by intersection score (decode order).
+struct GpePattern {
+    uint64_t erased_mask;
+    uint32_t nknown, nerased, nlevels, alpha;
+    uint8_t known[kGpeMaxKnown];
+    uint8_t erased[kGpeMaxErased];
+    uint32_t level_start[16];          // planes of level L: planes[level_start[L] .. level_start[L+1])
+    uint32_t planes_off;               // offset (in uint16) of this pattern's plane list in the plane pool
+    uint32_t pad_;
+    PermTab D[kGpeMaxErased][kGpeMaxKnown];  // U_erased[e] = sum_j D[e][j] * U_known[j]
+};
+
+struct GpeJob {
+    const uint8_t *in;     // node-strided input base
+    uint8_t *out;          // node-strided output base
+    uint64_t in_len;       // valid input bytes from `in` (zero beyond)
+    uint64_t out_len;      // output bytes kept from `out` (trim beyond)
+    uint32_t rot;          // rotation offset for the rotated side
+    uint32_t pattern;      // index into the pattern array
+};
+
+struct GpeArgs {
+    const GpeJob *jobs;
+    const GpePattern *patterns;
+    const uint16_t *plane_pool;
+    uint32_t njobs;
+    uint32_t words_per_stripe;
+    uint32_t groups_per_stripe;  // ceil(words_per_stripe / kGpeWords)
+    uint32_t cs, sc, q, t, k, nu, n, alpha;
+    uint64_t in_stride, out_stride;  // bytes between consecutive nodes on each side
+    uint32_t in_rotated, out_rotated;
+    uint64_t out_mask;               // internal nodes whose C is written to `out`
+    uint32_t qpow[16];               // q^i
+};
+
+// ---- repair engine ----
+struct RepPattern {
+    uint64_t erased_mask, aloof_mask;
+    uint32_t nknown, nerased, nlevels, beta;
+    uint32_t lost;                     // internal lost node
+    uint32_t pad_;
+    uint8_t known[kGpeMaxKnown];
+    uint8_t erased[kGpeMaxErased];
+    uint32_t level_start[16];          // over the repair-plane list
+    uint32_t planes_off;               // plane pool offset: beta repair planes in decode order
+    uint32_t pad2_;
+    PermTab D[kGpeMaxErased][kGpeMaxKnown];
+};
+
+struct RepJob {
+    const uint8_t *helper[kMaxNodes];  // per internal node: this stripe's beta sub-chunks (or null)
+    uint8_t *out;                      // lost chunk destination (chunk_size bytes)
+    uint32_t pattern;
+    uint32_t pad_;
+};
+
+struct RepArgs {
+    const RepJob *jobs;
+    const RepPattern *patterns;
+    const uint16_t *plane_pool;       // repair planes per pattern (decode order)
+    const uint16_t *plane_ind;        // per pattern: alpha entries, plane -> index in helper buffer
+    uint32_t njobs, words_per_stripe, groups_per_stripe;
+    uint32_t cs, sc, q, t, alpha;
+    uint32_t qpow[16];
+};
+
+constexpr int kGpeWords = 4;     // words (4 columns each) per GPE block
+constexpr int kGpePlaneThreads = 32;
+
+hipError_t launch_encode_rows(int k, const EncArgs &a, hipStream_t s);
+hipError_t launch_meta(const MetaJob *jobs, uint32_t njobs, uint32_t n, hipStream_t s);
+hipError_t launch_gpe(const GpeArgs &a, uint32_t max_erased, hipStream_t s);
+hipError_t launch_repair(const RepArgs &a, uint32_t max_erased, hipStream_t s);
+bool encode_rows_supported(int n, int k, int d);
+
+}  // namespace tec

@@ -1,0 +1,136 @@
+"""CPU-side checks of the product library (no GPU compute here):
+
+* libtapeec.so loads and exports every symbol include/tape_ec.h declares;
+* compute entry points fail loudly (NoDeviceError) without a device -- no CPU fallback;
+* host-only bookkeeping (geometry, rotation maps, metadata, repair plans, helper gather)
+  matches the oracle restatement of lib/slicer.
+"""
+import ctypes as C
+import random
+
+import pytest
+
+import tape_amd as T
+from tape_amd import _lib
+
+N = 20
+
+
+def test_exports_every_declared_symbol():
+    names = _lib.declared_symbols()
+    assert len(names) >= 30
+    so = C.CDLL(_lib.LIB_PATH)
+    missing = [n for n in names if not hasattr(so, n)]
+    assert not missing, missing
+
+
+def test_no_cpu_fallback():
+    if T.device_count() > 0:
+        pytest.skip("device present")
+    s = T.Slicer.clay_default()
+    with pytest.raises(T.NoDeviceError):
+        s.encode(b"hello world")
+    c = T.ClayCoder(20, 7, 16)
+    with pytest.raises(T.NoDeviceError):
+        c.encode(b"x" * 100)
+
+
+def test_invalid_params_assert():  # clay.rs:24-34 asserts
+    for n, k, d in [(7, 7, 6), (20, 0, 5), (20, 7, 7), (20, 7, 20)]:
+        with pytest.raises(AssertionError):
+            T.ClayCoder(n, k, d)
+
+
+def test_info_and_chunk_size(oracle):
+    for (n, k, d) in [(20, 7, 16), (20, 10, 19), (20, 5, 14), (12, 8, 11), (20, 7, 19)]:
+        c = T.ClayCoder(n, k, d)
+        o = oracle.OracleClay(n, k, d)
+        assert (c.k(), c.m(), c.n(), c.d(), c.alpha(), c.beta()) == (o.k, o.m, o.n, o.d, o.alpha, o.beta)
+        for ln in [0, 1, 999, 1400, 1401, 100_000, 194_304, 1_000_000, 10_000_000]:
+            assert c.chunk_size_for(ln) == o.chunk_size_for(ln)
+
+
+def test_geometry_matches_oracle(oracle):
+    s = T.Slicer.clay_default()
+    o = oracle.OracleClay(20, 7, 16)
+    for ln in [0, 1, 5000, 100_000, 1_000_000, 1_000_001, 1024 * 1024, 4 * 1024 * 1024, 64 * 1024 * 1024,
+               100_000_001]:
+        g = s.geometry(ln)
+        assert (g.stripe_size, g.num_stripes, g.chunk_size, g.slice_len) == oracle.geometry(o, ln)
+
+
+def test_rotation_maps_match_oracle(oracle):
+    for stripe in range(45):
+        for x in range(N):
+            for rot in (T.MappingStrategy.Identity, T.MappingStrategy.Rotated):
+                r = rot == T.MappingStrategy.Rotated
+                assert T.shard_to_slice(rot, N, stripe, x) == oracle.shard_to_slice(r, N, stripe, x)
+                assert T.slice_to_shard(rot, N, stripe, x) == oracle.slice_to_shard(r, N, stripe, x)
+
+
+def test_metadata_roundtrip():  # metadata.rs:115-151
+    m = T.SliceMetadata.new(12345, T.STRIPE_SIZES[0])
+    m.chunk_index = 42
+    b = m.to_bytes()
+    assert len(b) == 48 == T.SliceMetadata.SIZE
+    p = T.SliceMetadata.from_slice(bytes(100) + b)
+    assert (p.blob_len, p.stripe_size, p.version, p.chunk_index) == (12345, 100_000, 0, 42)
+    assert p.profile == T.EncodingProfile.clay_default()
+    with pytest.raises(T.DecodeError):
+        T.SliceMetadata.from_slice(bytes(47))
+    bad = T.SliceMetadata.new(1000, 999)
+    with pytest.raises(T.DecodeError):
+        T.SliceMetadata.from_slice(bad.to_bytes())
+
+
+@pytest.mark.parametrize("params", [(20, 7, 16), (20, 10, 19)])
+def test_repair_plans_match_oracle(oracle, params):
+    c = T.ClayCoder(*params)
+    o = oracle.OracleClay(*params)
+    rnd = random.Random(5)
+    for rotated in (False, True):
+        sl = T.Slicer(c, strategy=T.MappingStrategy.Rotated if rotated else T.MappingStrategy.Identity)
+        for trial in range(12):
+            lost = rnd.randrange(N)
+            others = [i for i in range(N) if i != lost]
+            navail = rnd.choice([c.d(), N - 1])
+            avail = sorted(rnd.sample(others, navail))
+            blob_len = rnd.choice([0, 1, 10_000, 300_000, 4 * 1024 * 1024])
+            stripe = T.pick_stripe_size(blob_len)
+            try:
+                cs, stripes = oracle.repair_plan(o, lost, avail, blob_len, stripe, rotated)
+            except ValueError:
+                with pytest.raises(T.RepairError):
+                    sl.repair_plan_from_params(lost, avail, blob_len, stripe)
+                continue
+            p = sl.repair_plan_from_params(lost, avail, blob_len, stripe)
+            assert p.chunk_size == cs and p.num_stripes == len(stripes)
+            assert p.sub_chunk_size == cs // o.alpha
+            for st, (s, ls, hs) in zip(p.stripes, stripes):
+                assert st.lost_shard == ls
+                assert [(h.slice, h.shard, h.sub_chunks) for h in st.helpers] == [tuple(x) for x in hs]
+
+
+def test_plan_repair_clay_level(oracle):
+    c = T.ClayCoder(20, 7, 16)
+    o = oracle.OracleClay(20, 7, 16)
+    for lost in range(N):
+        avail = [i for i in range(N) if i != lost]
+        assert c.plan_repair(lost, avail) == o.minimum_to_repair(lost, avail)
+    with pytest.raises(T.RepairError):
+        c.plan_repair(0, list(range(1, 16)))  # d-1 available
+
+
+def test_extract_repair_data_matches_oracle(oracle):
+    o = oracle.OracleClay(20, 7, 16)
+    data = oracle.splitmix64_bytes(9, 300_000).tobytes()
+    sl = oracle.slicer_encode(o, data)
+    s = T.Slicer.clay_default()
+    for lost in (0, 7, 19):
+        avail = [i for i in range(N) if i != lost]
+        p = s.repair_plan(lost, avail, sl[avail[0]])
+        cs, stripes = oracle.repair_plan(o, lost, avail, len(data), T.pick_stripe_size(len(data)), True)
+        for h in avail:
+            assert T.extract_repair_data(sl[h], p, h) == oracle.extract_repair_data(sl[h], cs, o.alpha, stripes, h)
+        with pytest.raises(T.RepairError):
+            T.extract_repair_data(sl[avail[0]][:100], p, avail[0])
