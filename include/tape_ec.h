@@ -61,6 +61,8 @@ const char *te_strerror(int status);
 int te_device_count(void);
 /* Bind the calling thread's engine context to a HIP device (default 0). */
 int te_set_device(int device);
+/* Detail of the last TE_ERR_HIP/OOM/NO_DEVICE on the calling thread (HIP error string). */
+const char *te_last_error_detail(void);
 /* Library build identification string. */
 const char *te_version(void);
 

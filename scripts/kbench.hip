@@ -1,0 +1,61 @@
+// kbench.hip -- ablation microbenchmark of the encode kernel (not part of the product build).
+// Builds enc_slab_kernel<7, MODE> variants over a device-resident 1024 x 4 MiB batch and
+// times each with hipEvents.  hipcc --offload-arch=gfx950 -O3 -std=c++20 -I tape_amd/csrc
+#include "../tape_amd/csrc/encode_slab.hip"
+#include <cstdio>
+#include <vector>
+using namespace tec;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+template <int MODE>
+float run(const EncArgs &a, uint32_t blocks, int reps) {
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+    hipLaunchKernelGGL((enc_slab_kernel<7, MODE, false>), dim3(blocks), dim3(640), 0, 0, a);
+    (void)hipEventRecord(e0, 0);
+    for (int r = 0; r < reps; r++) hipLaunchKernelGGL((enc_slab_kernel<7, MODE, false>), dim3(blocks), dim3(640), 0, 0, a);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    return ms / reps;
+}
+
+int main(int argc, char **argv) {
+    const int nobj = argc > 1 ? atoi(argv[1]) : 1024;
+    const size_t L = 4u << 20, S = 1000000, cs = 143000, sc = 1430, ns = 5, slen = ns * cs + 48;
+    uint8_t *din, *dout;
+    CK(hipMalloc(&din, nobj * L));
+    CK(hipMalloc(&dout, nobj * 20 * slen));
+    CK(hipMemset(din, 0x5a, nobj * L));
+    std::vector<EncJob> jobs;
+    for (int o = 0; o < nobj; o++)
+        for (size_t s = 0; s < ns; s++) {
+            EncJob j{};
+            j.src = din + (size_t)o * L + s * S;
+            j.src_len = std::min<size_t>(S, L - s * S);
+            j.dst = dout + (size_t)o * 20 * slen + s * cs;
+            j.rot = (uint32_t)((s * 7) % 20);
+            j.dst_skew = (uint32_t)(s * cs);
+            jobs.push_back(j);
+        }
+    EncJob *dj;
+    CK(hipMalloc(&dj, jobs.size() * sizeof(EncJob)));
+    CK(hipMemcpy(dj, jobs.data(), jobs.size() * sizeof(EncJob), hipMemcpyHostToDevice));
+    EncArgs a{};
+    a.jobs = dj; a.njobs = (uint32_t)jobs.size(); a.words_per_stripe = (sc + 3) / 4;
+    a.groups_per_stripe = (a.words_per_stripe + 63) / 64; a.cs = cs; a.sc = sc; a.slice_len = slen; a.n = 20;
+    const uint32_t blocks = a.njobs * a.groups_per_stripe;
+    const double alg = (double)nobj * (L + 20.0 * slen);
+    const int reps = 5;
+    float t;
+    t = run<0>(a, blocks, reps); printf("mode0 full            %8.3f ms  %7.1f GB/s\n", t, alg / t / 1e6);
+    t = run<1>(a, blocks, reps); printf("mode1 no-stores       %8.3f ms\n", t);
+    t = run<2>(a, blocks, reps); printf("mode2 no-GF-math      %8.3f ms  %7.1f GB/s\n", t, alg / t / 1e6);
+    t = run<4>(a, blocks, reps); printf("mode4 no-LDS-exchange %8.3f ms  %7.1f GB/s\n", t, alg / t / 1e6);
+    t = run<6>(a, blocks, reps); printf("mode6 no-GF no-LDS    %8.3f ms  %7.1f GB/s\n", t, alg / t / 1e6);
+    t = run<3>(a, blocks, reps); printf("mode3 no-st no-GF     %8.3f ms\n", t);
+    t = run<7>(a, blocks, reps); printf("mode7 loads only      %8.3f ms\n", t);
+    return 0;
+}

@@ -3,9 +3,8 @@
 // A "word" is 4 byte-columns of one sub-chunk (cols c..c+3).  Sub-chunks are sc bytes with
 // sc = chunk_size/alpha, always even but only 2-aligned (sc = 1,430 for 1 MB stripes), so a
 // word sits at an address that is 0 or 2 mod 4.  Aligned words move as one dword; the others as
-// two 16-bit halves (never an unaligned dword).  The last word of a sub-chunk is shifted back
-// to end at sc (it overlaps its neighbour; both lanes write identical bytes).  When sc == 2 a
-// word carries only 2 columns.
+// two 16-bit halves (never an unaligned dword).  When sc = 2 mod 4 the last word of a
+// sub-chunk carries only 2 columns, so alignment stays uniform across a wave.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -19,9 +18,8 @@ struct WordPos {
 
 __device__ __forceinline__ WordPos word_pos(uint32_t w, uint32_t sc) {
     WordPos p;
-    p.nc = sc >= 4 ? 4u : sc;
-    const uint32_t c = w * 4u;
-    p.c = c + p.nc <= sc ? c : sc - p.nc;
+    p.c = w * 4u;
+    p.nc = p.c + 4u <= sc ? 4u : sc - p.c;
     return p;
 }
 
@@ -67,6 +65,44 @@ __device__ __forceinline__ void st_word_trim(uint8_t *__restrict__ base, uint64_
     }
     for (uint32_t i = 0; i < nc; i++)
         if (off + i < limit) base[off + i] = (uint8_t)(v >> (8 * i));
+}
+
+// Wave-uniform access: `ub` (uniform base, SGPR) + the lane's 32-bit column offset.  `al` is the
+// uniform alignment of ub (ub & 3): 0 -> one dword, 2 -> two 16-bit halves, odd -> bytes.
+#define TEC_GLOBAL __attribute__((address_space(1)))
+typedef TEC_GLOBAL uint8_t g_u8;
+typedef TEC_GLOBAL uint16_t g_u16;
+typedef TEC_GLOBAL uint32_t g_u32;
+
+__device__ __forceinline__ uint32_t ld_u(const uint8_t *ub_, uint32_t col, uint32_t al) {
+    const g_u8 *ub = (const g_u8 *)ub_;
+    if (al == 0) return *(const g_u32 *)(ub + col);
+    if (al == 2) {
+        const uint32_t lo = *(const g_u16 *)(ub + col);
+        const uint32_t hi = *(const g_u16 *)(ub + col + 2);
+        return lo | (hi << 16);
+    }
+    const g_u8 *p = ub + col;
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+__device__ __forceinline__ void st_u(uint8_t *ub_, uint32_t col, uint32_t al, uint32_t v) {
+    g_u8 *ub = (g_u8 *)ub_;
+    if (al == 0) {
+        *(g_u32 *)(ub + col) = v;
+    } else if (al == 2) {
+        *(g_u16 *)(ub + col) = (uint16_t)v;
+        *(g_u16 *)(ub + col + 2) = (uint16_t)(v >> 16);
+    } else {
+        g_u8 *p = ub + col;
+        p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
+    }
+}
+
+// Workgroup barrier for LDS-only hand-offs: waits for this wave's LDS operations, not for its
+// global loads/stores (a __syncthreads() is a full fence and would drain vmcnt every plane).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // XCD-aware block remap: blocks b and b+8 share an XCD (round-robin dispatch), so give each

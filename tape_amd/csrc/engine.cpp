@@ -7,6 +7,7 @@
 // TE_ERR_NO_DEVICE.
 #include <hip/hip_runtime.h>
 #include <string.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <map>
 #include <mutex>
@@ -22,8 +23,11 @@ namespace {
 
 constexpr size_t kStripeSizes[3] = {100000, 1000000, 10000000};  // adaptive.rs:15-19
 
+thread_local char g_last_error[256] = "";
+
 int hip_status(hipError_t e) {
     if (e == hipSuccess) return TE_OK;
+    snprintf(g_last_error, sizeof(g_last_error), "%s (%d)", hipGetErrorString(e), (int)e);
     if (e == hipErrorOutOfMemory) return TE_ERR_OUT_OF_MEMORY;
     if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return TE_ERR_NO_DEVICE;
     return TE_ERR_HIP;
@@ -210,6 +214,8 @@ const char *te_strerror(int s) {
 
 int te_device_count(void) { return device_count(); }
 
+const char *te_last_error_detail(void) { return g_last_error; }
+
 int te_set_device(int device) {
     if (device < 0 || device >= device_count()) return TE_ERR_NO_DEVICE;
     TE_HIP(hipSetDevice(device));
@@ -337,7 +343,12 @@ namespace {
 
 struct GeomKey {
     uint64_t cs, slice_len;
-    bool operator<(const GeomKey &o) const { return cs != o.cs ? cs < o.cs : slice_len < o.slice_len; }
+    bool masked;  // stripe data end not dword aligned -> masked kernel variant
+    bool operator<(const GeomKey &o) const {
+        if (cs != o.cs) return cs < o.cs;
+        if (slice_len != o.slice_len) return slice_len < o.slice_len;
+        return masked < o.masked;
+    }
 };
 
 int ensure_stream(te_clay *c) {
@@ -355,6 +366,7 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
     const int rotated = cfg ? cfg->rotated : 0;
     std::map<GeomKey, std::vector<EncJob>> groups;
     std::vector<MetaJob> metas;
+
     for (size_t i = 0; i < nobj; i++) {
         const te_object &o = objs[i];
         size_t S, ns, cs, slice_len;
@@ -370,7 +382,6 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
             S = g.stripe_size; ns = g.num_stripes; cs = g.chunk_size; slice_len = g.slice_len;
         }
         if (cs % (size_t)h.alpha || slice_len > 0xffffffffull || cs > 0xffffffffull) return TE_ERR_TOO_MUCH_DATA;
-        auto &jobs = groups[GeomKey{cs, slice_len}];
         for (size_t st = 0; st < ns; st++) {
             EncJob j{};
             const uint64_t start = (uint64_t)st * S;
@@ -378,7 +389,9 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
             j.src_len = o.blob_len == 0 ? 0 : std::min<uint64_t>(S, o.blob_len - start);
             j.dst = d_out + o.out_off + st * cs;
             j.rot = rotated ? (uint32_t)((st * TE_ROTATION_STEP) % n) : 0u;
-            jobs.push_back(j);
+            j.dst_skew = (uint32_t)(st * cs);
+            const bool masked = ((reinterpret_cast<uintptr_t>(j.src) & 3u) + j.src_len) % 4 != 0;
+            groups[GeomKey{cs, slice_len, masked}].push_back(j);
         }
         if (!raw) {
             MetaJob m{};
@@ -406,7 +419,7 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
     std::vector<uint16_t> pool;
     std::vector<GpeJob> gjobs;
     std::vector<size_t> gjob_off;
-    if (!c->fast_encode) {
+    {
         uint64_t mask = 0;
         for (int i = h.k + h.nu; i < h.qt; i++) mask |= 1ull << i;
         if (!h.gpe_pattern(mask, pat, pool)) return TE_ERR_UNSUPPORTED;
@@ -425,36 +438,47 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
     int r = A.upload(s);
     if (r) return r;
     if (!metas.empty()) TE_HIP(launch_meta(A.at<MetaJob>(meta_off), (uint32_t)metas.size(), (uint32_t)n, s));
+    auto gpe_args = [&](size_t gi, const Launch &L, uint32_t word_base, uint32_t word_end) {
+        const uint32_t cs = (uint32_t)L.key.cs, sc = cs / (uint32_t)h.alpha;
+        (void)sc;
+        GpeArgs a{};
+        a.jobs = A.at<GpeJob>(gjob_off[gi]);
+        a.patterns = A.at<GpePattern>(pat_off);
+        a.plane_pool = A.at<uint16_t>(pool_off);
+        a.njobs = (uint32_t)L.count;
+        a.word_base = word_base;
+        a.word_end = word_end;
+        a.groups_per_stripe = (word_end - word_base + kGpeWords - 1) / kGpeWords;
+        a.cs = cs; a.sc = cs / (uint32_t)h.alpha; a.q = h.q; a.t = h.t; a.k = h.k; a.nu = h.nu; a.n = n;
+        a.alpha = h.alpha;
+        a.in_stride = cs; a.out_stride = L.key.slice_len;
+        a.in_rotated = 0; a.out_rotated = 1;
+        a.out_mask = 0;
+        for (int i = 0; i < h.qt; i++)
+            if (h.int_to_ext(i) >= 0) a.out_mask |= 1ull << i;
+        for (int i = 0; i < 16; i++) a.qpow[i] = h.qpow[i];
+        return a;
+    };
     size_t gi = 0;
     for (const Launch &L : launches) {
         const uint32_t cs = (uint32_t)L.key.cs, sc = cs / (uint32_t)h.alpha;
-        const uint32_t wps = sc >= 4 ? (sc + 3) / 4 : 1;
-        if (c->fast_encode) {
+        const uint32_t wps = (sc + 3) / 4;   // words incl. a 2-column tail when sc % 4 == 2
+        const uint32_t full = sc / 4;        // full 4-column words
+        // fast kernel addresses an object's slices with 31-bit buffer offsets
+        if (c->fast_encode && (uint64_t)n * L.key.slice_len < 0x7fffffffull) {
+            (void)full;
             EncArgs a{};
             a.jobs = A.at<EncJob>(L.off);
-            a.total_words = (uint64_t)L.count * wps;
+            a.njobs = (uint32_t)L.count;
+            a.groups_per_stripe = (wps + 63) / 64;
             a.words_per_stripe = wps;
             a.cs = cs;
             a.sc = sc;
             a.slice_len = (uint32_t)L.key.slice_len;
             a.n = (uint32_t)n;
-            TE_HIP(launch_encode_rows(h.k, a, s));
+            TE_HIP(launch_encode_rows(h.k, L.key.masked, a, s));
         } else {
-            GpeArgs a{};
-            a.jobs = A.at<GpeJob>(gjob_off[gi]);
-            a.patterns = A.at<GpePattern>(pat_off);
-            a.plane_pool = A.at<uint16_t>(pool_off);
-            a.njobs = (uint32_t)L.count;
-            a.words_per_stripe = wps;
-            a.groups_per_stripe = (wps + kGpeWords - 1) / kGpeWords;
-            a.cs = cs; a.sc = sc; a.q = h.q; a.t = h.t; a.k = h.k; a.nu = h.nu; a.n = n; a.alpha = h.alpha;
-            a.in_stride = cs; a.out_stride = L.key.slice_len;
-            a.in_rotated = 0; a.out_rotated = 1;
-            a.out_mask = 0;
-            for (int i = 0; i < h.qt; i++)
-                if (h.int_to_ext(i) >= 0) a.out_mask |= 1ull << i;
-            for (int i = 0; i < 16; i++) a.qpow[i] = h.qpow[i];
-            TE_HIP(launch_gpe(a, (uint32_t)pat.nerased, s));
+            TE_HIP(launch_gpe(gpe_args(gi, L, 0, wps), (uint32_t)pat.nerased, s));
         }
         gi++;
     }
@@ -563,7 +587,8 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         a.patterns = A.at<GpePattern>(pat_off);
         a.plane_pool = A.at<uint16_t>(pool_off);
         a.njobs = (uint32_t)groups[o.first].size();
-        a.words_per_stripe = wps;
+        a.word_base = 0;
+        a.word_end = wps;
         a.groups_per_stripe = (wps + kGpeWords - 1) / kGpeWords;
         a.cs = (uint32_t)cs; a.sc = sc; a.q = h.q; a.t = h.t; a.k = h.k; a.nu = h.nu; a.n = n; a.alpha = h.alpha;
         a.in_stride = group_in_stride[o.first];

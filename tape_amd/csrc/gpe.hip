@@ -24,8 +24,8 @@ __global__ void __launch_bounds__(kGpeWords * kGpePlaneThreads) gpe_kernel(GpeAr
     const uint32_t job = blockIdx.x / a.groups_per_stripe;
     const uint32_t grp = blockIdx.x - job * a.groups_per_stripe;
     const uint32_t wi = threadIdx.x % kGpeWords, pt = threadIdx.x / kGpeWords;
-    uint32_t w = grp * kGpeWords + wi;
-    if (w >= a.words_per_stripe) w = a.words_per_stripe - 1;
+    uint32_t w = a.word_base + grp * kGpeWords + wi;
+    if (w >= a.word_end) w = a.word_end - 1;
     const GpeJob J = a.jobs[job];
     const GpePattern &PT = a.patterns[J.pattern];
     const WordPos wp = word_pos(w, a.sc);
@@ -40,7 +40,7 @@ __global__ void __launch_bounds__(kGpeWords * kGpePlaneThreads) gpe_kernel(GpeAr
         const uint32_t z = i / t, y = i - z * t;
         dig[i] = (uint8_t)((z / a.qpow[t - 1 - y]) % q);
     }
-    __syncthreads();
+    lds_barrier();
 
     auto ext_of = [&](uint32_t node) -> int {
         return node < a.k ? (int)node : (node < a.k + a.nu ? -1 : (int)(node - a.nu));
@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(kGpeWords * kGpePlaneThreads) gpe_kernel(GpeAr
             for (int e = 0; e < MAXE; e++)
                 if ((uint32_t)e < ner) slot(Ur, e, z) = acc[e];
         }
-        __syncthreads();
+        lds_barrier();
         // ---- phase B: re-couple the erased nodes of this level ----
         for (uint32_t pi = ls + pt; pi < le; pi += kGpePlaneThreads) {
             const uint32_t z = planes[pi];
@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(kGpeWords * kGpePlaneThreads) gpe_kernel(GpeAr
                 if ((a.out_mask >> node) & 1ull) store_out(node, z, cval);
             }
         }
-        __syncthreads();
+        lds_barrier();
     }
 }
 
@@ -160,7 +160,7 @@ __global__ void __launch_bounds__(kGpeWords * kGpePlaneThreads) repair_kernel(Re
         const uint32_t z = i / t, y = i - z * t;
         dig[i] = (uint8_t)((z / a.qpow[t - 1 - y]) % q);
     }
-    __syncthreads();
+    lds_barrier();
 
     const uint16_t *pind = a.plane_ind + (size_t)J.pattern * alpha;
     auto load_h = [&](uint32_t node, uint32_t ri) -> uint32_t {
@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(kGpeWords * kGpePlaneThreads) repair_kernel(Re
                 }
             }
         }
-        __syncthreads();
+        lds_barrier();
     }
 }
 

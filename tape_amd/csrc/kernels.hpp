@@ -12,12 +12,14 @@ struct EncJob {
     uint8_t *dst;         // object's slice-0 base + stripe*chunk_size
     uint64_t src_len;     // valid bytes of the stripe (rest is zero padding)
     uint32_t rot;         // rotation offset (stripe*7) % n, 0 for identity mapping
-    uint32_t pad_;
+    uint32_t dst_skew;    // stripe*chunk_size: dst - (object's slice-0 base)
+    uint64_t pad_;
 };
 
 struct EncArgs {
     const EncJob *jobs;
-    uint64_t total_words;  // njobs * words_per_stripe
+    uint32_t njobs;
+    uint32_t groups_per_stripe;  // ceil(words_per_stripe / 64): workgroups per stripe
     uint32_t words_per_stripe;
     uint32_t cs;           // chunk size
     uint32_t sc;           // sub-chunk size
@@ -63,8 +65,8 @@ struct GpeArgs {
     const GpePattern *patterns;
     const uint16_t *plane_pool;
     uint32_t njobs;
-    uint32_t words_per_stripe;
-    uint32_t groups_per_stripe;  // ceil(words_per_stripe / kGpeWords)
+    uint32_t word_base, word_end;  // words [word_base, word_end) of each stripe are processed
+    uint32_t groups_per_stripe;  // ceil((word_end - word_base) / kGpeWords)
     uint32_t cs, sc, q, t, k, nu, n, alpha;
     uint64_t in_stride, out_stride;  // bytes between consecutive nodes on each side
     uint32_t in_rotated, out_rotated;
@@ -106,7 +108,7 @@ struct RepArgs {
 constexpr int kGpeWords = 4;     // words (4 columns each) per GPE block
 constexpr int kGpePlaneThreads = 32;
 
-hipError_t launch_encode_rows(int k, const EncArgs &a, hipStream_t s);
+hipError_t launch_encode_rows(int k, bool masked, const EncArgs &a, hipStream_t s);
 hipError_t launch_meta(const MetaJob *jobs, uint32_t njobs, uint32_t n, hipStream_t s);
 hipError_t launch_gpe(const GpeArgs &a, uint32_t max_erased, hipStream_t s);
 hipError_t launch_repair(const RepArgs &a, uint32_t max_erased, hipStream_t s);

@@ -39,7 +39,8 @@ class EngineError(RuntimeError):
 
     def __init__(self, code: int, msg: str | None = None):
         self.code = code
-        super().__init__(msg or f"{_lib.strerror(code)} (status {code})")
+        detail = lib.te_last_error_detail().decode() if code in (_lib.TE_ERR_HIP, _lib.TE_ERR_OUT_OF_MEMORY) else ""
+        super().__init__(msg or f"{_lib.strerror(code)} (status {code}){': ' + detail if detail else ''}")
 
 
 class NoDeviceError(EngineError):
