@@ -36,7 +36,7 @@ def splitmix_fill(torch, out_u8, first_obj: int, nobj: int, obj_len: int, seed: 
     """Device-side SplitMix64 stream per object: byte j of object i = word floor(j/8) of
     SplitMix64(seed ^ i), little-endian.  Same stream as oracle.splitmix64_bytes.
     Vectorised over 64 objects per pass (few kernels, so profiles stay small)."""
-    words = obj_len // 8
+    words = (obj_len + 7) // 8
     G = -7046029254386353131  # 0x9E3779B97F4A7C15 as int64
     M1 = -4658895280553007687  # 0xBF58476D1CE4E5B9
     M2 = -7723592293110705685  # 0x94D049BB133111EB
@@ -57,8 +57,37 @@ def splitmix_fill(torch, out_u8, first_obj: int, nobj: int, obj_len: int, seed: 
         z = (z ^ lsr(z, 30)) * M1
         z = (z ^ lsr(z, 27)) * M2
         z = z ^ lsr(z, 31)
-        view[c0:c1, :words * 8].copy_(z.view(torch.uint8).view(c1 - c0, words * 8))
+        view[c0:c1].copy_(z.view(torch.uint8).view(c1 - c0, words * 8)[:, :obj_len])
         del z
+
+
+def dist_setup(torch, dist, backend: str):
+    """One process per GPU (torchrun env).  Objects are partitioned, so the process group is used
+    only for the barrier and the max-over-ranks timing -- never on the data path."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return world, rank, local
+
+
+def rank_objects(rank: int, nobj: int) -> tuple[int, int]:
+    """Contiguous global object range [first, first + nobj) of this rank (weak scaling)."""
+    return rank * nobj, rank * nobj + nobj
+
+
+def max_over_ranks(torch, dist, world: int, seconds: float, dev) -> float:
+    if world <= 1:
+        return seconds
+    t = torch.tensor([seconds], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def main():
@@ -71,6 +100,9 @@ def main():
     ap.add_argument("--mode", choices=["encode", "repair", "decode"], default="encode")
     ap.add_argument("--cpu-sample", type=int, default=96, help="objects in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity cores)")
+    ap.add_argument("--copy-objects", type=int, default=256,
+                    help="objects in the copy-inclusive (pinned host -> host) leg, encode mode (0 = skip)")
+    ap.add_argument("--copy-steps", type=int, default=4)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -80,13 +112,7 @@ def main():
     import tape_amd as T
     from tape_amd import batch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    world, rank, local = dist_setup(torch, dist, "nccl")
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
     T.lib.te_set_device(dev.index)
@@ -95,7 +121,7 @@ def main():
     slicer = T.Slicer.clay_default()
     g = slicer.geometry(L)
     per = N * g.slice_len
-    first = rank * nobj
+    first, _ = rank_objects(rank, nobj)
     d_in = torch.empty(nobj * L, dtype=torch.uint8, device=dev)
     splitmix_fill(torch, d_in, first, nobj, L)
     d_out = torch.empty(nobj * per, dtype=torch.uint8, device=dev)
@@ -163,15 +189,24 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     launch_ms = [a.elapsed_time(b) for a, b in ev]
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(torch, dist, world, elapsed, dev)
 
     total_objs = nobj * world * args.steps
     gib_s = total_objs * L / elapsed / 2**30
     avg_launch_s = sum(launch_ms) / len(launch_ms) / 1e3
     achieved = (unit_bytes or 0) * nobj / avg_launch_s / 1e9 if unit_bytes else None
+
+    verified = None  # the timed outputs, checked on the device against what they must equal
+    if args.mode == "decode":
+        verified = bool(torch.equal(d_dec, d_in))
+    elif args.mode == "repair":
+        sl = g.slice_len
+        ref = torch.stack([d_out[i * per + (i % N) * sl:i * per + (i % N + 1) * sl] for i in range(nobj)])
+        verified = bool(torch.equal(d_rep.view(nobj, sl), ref))
+        del ref
+    copy_inc = None
+    if args.mode == "encode" and args.copy_objects > 0:
+        copy_inc = copy_inclusive(args, torch, dist, world, slicer, batch, d_in, d_out, per, L, dev)
 
     cpu = None
     if rank == 0 and args.cpu_sample > 0 and args.mode == "encode":
@@ -209,10 +244,37 @@ def main():
                          "alg_bytes_per_launch": unit_bytes * nobj if unit_bytes else None,
                          "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
             "cpu_baseline": cpu,
+            "copy_inclusive": copy_inc,
+            "outputs_verified": verified,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def copy_inclusive(args, torch, dist, world, slicer, batch, d_in, d_out, per, L, dev):
+    """Copy-inclusive encode rate: pinned host object bytes in, pinned host
+    slices out, through te_encode_batch_host (3-slot H2D / kernel / D2H pipeline).  Reported
+    beside `value`, never as it.  Every rank runs it at once (max over ranks), so at N>1 it
+    includes the host-memory / PCIe contention of the node."""
+    m = min(args.copy_objects, args.objects)
+    h_in = torch.empty(m * L, dtype=torch.uint8).pin_memory()
+    h_in.copy_(d_in[:m * L])
+    h_out = torch.empty(m * per, dtype=torch.uint8).pin_memory()
+    objs = [(i * L, L, i * per, 0) for i in range(m)]
+    batch.encode_batch_host(slicer, h_in, objs, h_out)  # warm-up (pipeline buffers)
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter()
+    for _ in range(args.copy_steps):
+        batch.encode_batch_host(slicer, h_in, objs, h_out)
+    el = time.perf_counter() - t
+    el = max_over_ranks(torch, dist, world, el, dev)
+    ok = bool(torch.equal(h_out[:per], d_out[:per].cpu()))  # same bytes as the device-resident run
+    return {"value": round(m * world * args.copy_steps * L / el / 2**30, 3), "unit": "GiB/s",
+            "objects_per_gpu": m, "steps": args.copy_steps, "pinned": True,
+            "ms_per_step": round(el / args.copy_steps * 1e3, 3),
+            "h2d_plus_d2h_bytes_per_object": L + per, "matches_device_resident": ok}
 
 
 def cpu_baseline(args, np, torch, d_in, d_out, per, L):

@@ -190,6 +190,15 @@ typedef struct te_object {
 int te_encode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data,
                            const te_object *objs, size_t nobj, uint8_t *d_out, void *hip_stream);
 
+/* Batched Slicer::encode HOST -> HOST: the shape of the sdk stream writer's encode stage
+ * (sdk/src/stream/write.rs:332-362: object bytes in, n slices per object out).  Offsets in
+ * `objs` are relative to h_data / h_out.  Objects are pipelined through the device in windows
+ * of at most `window_bytes` (input + output; 0 = 1 GiB) over three streams, so the H2D copy of
+ * one window, the kernels of the next and the D2H copy of a third overlap.  h_data/h_out
+ * should be pinned (hipHostMalloc / hipHostRegister) for full PCIe rate.  Synchronous. */
+int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data,
+                         const te_object *objs, size_t nobj, uint8_t *h_out, size_t window_bytes);
+
 typedef struct te_decode_object {
     uint64_t slices_off;  /* slice i at d_slices + slices_off + i*slice_len */
     uint64_t slice_len;

@@ -125,6 +125,7 @@ def _load() -> C.CDLL:
         "te_extract_repair_data": (i, [vp, u8p, sz, u32, u8p, sz, szp]),
         "te_slicer_repair": (i, [vp, vp, pp, szp, u8p, u8p, sz]),
         "te_encode_batch_device": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz, vp, vp]),
+        "te_encode_batch_host": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz, vp, sz]),
         "te_decode_batch_device": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_decode_object), u8p, sz,
                                        vp, vp]),
         "te_repair_batch_device": (i, [vp, vp, C.POINTER(te_repair_object), sz, vp, vp]),

@@ -27,6 +27,23 @@ def encode_batch(slicer: Slicer, data, objs: list[tuple[int, int, int, int]], ou
     _check(r, "encode")
 
 
+def encode_batch_host(slicer: Slicer, data, objs: list[tuple[int, int, int, int]], out, window_bytes: int = 0) -> None:
+    """Host -> host batched encode (te_encode_batch_host): data/out are host buffers (numpy arrays
+    or CPU tensors, pinned for full PCIe rate); objs as for encode_batch, offsets into data/out."""
+    arr = (_lib.te_object * len(objs))(*[_lib.te_object(*o) for o in objs])
+    cfg = slicer._cfg()
+    r = lib.te_encode_batch_host(slicer.coder.handle, C.byref(cfg), C.c_void_p(_host_ptr(data)), arr, len(objs),
+                                 C.c_void_p(_host_ptr(out)), window_bytes)
+    _check(r, "encode")
+
+
+def _host_ptr(buf) -> int:
+    if hasattr(buf, "data_ptr"):
+        assert not buf.is_cuda, "host buffer expected"
+        return buf.data_ptr()
+    return buf.ctypes.data
+
+
 def decode_batch(slicer: Slicer, slices, objs: list[tuple[int, int, int, int]], metas: bytes, out,
                  stream=None) -> None:
     """objs: (slices_off, slice_len, avail_mask, out_off); metas: nobj*48 metadata bytes (host)."""

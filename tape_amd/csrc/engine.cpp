@@ -177,6 +177,14 @@ struct te_clay {
     hipStream_t stream = nullptr;  // for the synchronous host-buffer entry points
     Arena enc, dec, rep;
     DevBuf io_in, io_out;          // staging for host-buffer entry points
+    // te_encode_batch_host pipeline: kPipe slots, each with its own stream, descriptor arena
+    // and device window buffers, so window w+1's H2D overlaps window w's kernel and D2H.
+    static constexpr int kPipe = 3;
+    struct Slot {
+        hipStream_t s = nullptr;
+        Arena arena;
+        DevBuf in, out;
+    } pipe[kPipe];
 };
 
 struct te_repair_plan {
@@ -255,6 +263,13 @@ void te_clay_free(te_clay *c) {
         c->io_in.release();
         c->io_out.release();
         if (c->stream) (void)hipStreamDestroy(c->stream);
+        for (auto &sl : c->pipe) {
+            if (sl.s) (void)hipStreamSynchronize(sl.s);
+            sl.arena.release();
+            sl.in.release();
+            sl.out.release();
+            if (sl.s) (void)hipStreamDestroy(sl.s);
+        }
     }
     delete c;
 }
@@ -360,7 +375,7 @@ int ensure_stream(te_clay *c) {
 // Enqueue the encode of a batch.  raw = ClayCoder::encode semantics (no slicing/rotation/meta,
 // slices are the n chunks of one padded input).
 int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, const te_object *objs,
-                   size_t nobj, uint8_t *d_out, hipStream_t s, bool raw) {
+                   size_t nobj, uint8_t *d_out, hipStream_t s, bool raw, Arena *arena = nullptr) {
     const ClayHost &h = c->h;
     const int n = h.n;
     const int rotated = cfg ? cfg->rotated : 0;
@@ -407,7 +422,7 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
         }
     }
     // descriptor image
-    Arena &A = c->enc;
+    Arena &A = arena ? *arena : c->enc;
     A.img.clear();
     struct Launch { GeomKey key; size_t off, count; };
     std::vector<Launch> launches;
@@ -737,6 +752,77 @@ int te_encode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *
     if (device_count() <= 0) return TE_ERR_NO_DEVICE;
     std::lock_guard<std::mutex> lk(c->mu);
     return encode_enqueue(c, cfg, d_data, objs, nobj, d_out, (hipStream_t)stream, false);
+}
+
+int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data, const te_object *objs,
+                         size_t nobj, uint8_t *h_out, size_t window_bytes) {
+    if (!c || !cfg || (!objs && nobj) || (nobj && (!h_data || !h_out))) return TE_ERR_INVALID_ARG;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    if (window_bytes == 0) window_bytes = (size_t)1 << 30;
+    std::vector<uint64_t> out_bytes(nobj);
+    for (size_t i = 0; i < nobj; i++) {
+        te_geometry g;
+        te_slicer_geometry(c, objs[i].blob_len, &g);
+        out_bytes[i] = (uint64_t)c->h.n * g.slice_len;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    for (auto &sl : c->pipe)
+        if (!sl.s) TE_HIP(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
+    // Copy runs: consecutive objects contiguous on the host are moved with one DMA.
+    struct Run { uint64_t host, dev, len; };
+    auto add_run = [](std::vector<Run> &v, uint64_t host, uint64_t dev, uint64_t len) {
+        if (!len) return;
+        if (!v.empty() && v.back().host + v.back().len == host && v.back().dev + v.back().len == dev)
+            v.back().len += len;
+        else
+            v.push_back({host, dev, len});
+    };
+    int rc = TE_OK;
+    size_t i = 0, w = 0;
+    std::vector<te_object> local;
+    std::vector<Run> hin, hout;
+    while (i < nobj && rc == TE_OK) {
+        // window [i, j): at least one object, in + out bytes within window_bytes
+        size_t j = i;
+        uint64_t in_sz = 0, out_sz = 0;
+        while (j < nobj && (j == i || in_sz + out_sz + objs[j].blob_len + out_bytes[j] <= window_bytes)) {
+            in_sz += objs[j].blob_len;
+            out_sz += out_bytes[j];
+            j++;
+        }
+        te_clay::Slot &sl = c->pipe[w % te_clay::kPipe];
+        if ((rc = hip_status(sl.in.ensure(in_sz + 16))) || (rc = hip_status(sl.out.ensure(out_sz)))) break;
+        local.clear();
+        hin.clear();
+        hout.clear();
+        uint64_t din = 0, dout = 0;
+        for (size_t o = i; o < j; o++) {
+            local.push_back(te_object{din, objs[o].blob_len, dout, objs[o].chunk_index});
+            add_run(hin, objs[o].data_off, din, objs[o].blob_len);
+            add_run(hout, objs[o].out_off, dout, out_bytes[o]);
+            din += objs[o].blob_len;
+            dout += out_bytes[o];
+        }
+        for (const Run &r : hin)
+            if ((rc = hip_status(hipMemcpyAsync(sl.in.as<uint8_t>() + r.dev, h_data + r.host, r.len,
+                                                hipMemcpyHostToDevice, sl.s))))
+                break;
+        if (rc) break;
+        rc = encode_enqueue(c, cfg, sl.in.as<uint8_t>(), local.data(), local.size(), sl.out.as<uint8_t>(), sl.s,
+                            false, &sl.arena);
+        if (rc) break;
+        for (const Run &r : hout)
+            if ((rc = hip_status(hipMemcpyAsync(h_out + r.host, sl.out.as<uint8_t>() + r.dev, r.len,
+                                                hipMemcpyDeviceToHost, sl.s))))
+                break;
+        i = j;
+        w++;
+    }
+    for (auto &sl : c->pipe) {
+        const int r2 = hip_status(hipStreamSynchronize(sl.s));
+        if (rc == TE_OK) rc = r2;
+    }
+    return rc;
 }
 
 int te_decode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices, const te_decode_object *objs,

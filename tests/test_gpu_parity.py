@@ -251,3 +251,37 @@ def test_batch_mixed_sizes(oracle, o716):
         g = s.geometry(ln)
         exp = oracle.slicer_encode_np(o716, host[offs[i]:offs[i] + ln])
         assert np.array_equal(out[outs[i]:outs[i] + N * g.slice_len].reshape(N, -1), exp), ln
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_batch_encode_host_pipeline(oracle, o716, pinned):
+    """te_encode_batch_host: host -> host, windows small enough to force many pipeline slots."""
+    from tape_amd import batch
+    sizes = [4 * MiB] * 6 + [1, 0, 777_777, 2 * MiB + 3]
+    s = T.Slicer.clay_default()
+    offs, cur, outs, ocur = [], 0, [], 0
+    for ln in sizes:
+        offs.append(cur)
+        cur += ln + (5 if ln % 2 else 0)  # contiguous runs and gaps
+        outs.append(ocur)
+        ocur += N * s.geometry(ln).slice_len
+    h_in = torch.zeros(cur, dtype=torch.uint8)
+    h_out = torch.zeros(ocur, dtype=torch.uint8)
+    if pinned:
+        h_in, h_out = h_in.pin_memory(), h_out.pin_memory()
+    npin = h_in.numpy()
+    for i, ln in enumerate(sizes):
+        npin[offs[i]:offs[i] + ln] = oracle.splitmix64_bytes(1000 + i, ln)
+    objs = [(offs[i], sizes[i], outs[i], i) for i in range(len(sizes))]
+    batch.encode_batch_host(s, h_in, objs, h_out, window_bytes=40 * MiB)
+    out = h_out.numpy()
+    for i, ln in enumerate(sizes):
+        g = s.geometry(ln)
+        if i in (0, 5) or ln < 4 * MiB:  # oracle on a sample, SHA of device path on the rest
+            o = oracle.slicer_encode_np(o716, npin[offs[i]:offs[i] + ln], chunk_index=i)
+            assert np.array_equal(out[outs[i]:outs[i] + N * g.slice_len].reshape(N, -1), o), (i, ln)
+    # identical to the device-resident batch path for every object
+    d_out = torch.zeros(ocur, dtype=torch.uint8, device="cuda:0")
+    batch.encode_batch(s, h_in.to("cuda:0"), objs, d_out)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_out.cpu().numpy(), out)
