@@ -8,17 +8,27 @@ using namespace tec;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
+__global__ void fill_random(uint32_t *p, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = (uint32_t)(z ^ (z >> 31));
+    }
+}
+
 template <int MODE>
-float run(const EncArgs &a, uint32_t blocks, int reps) {
+float run(const EncArgs &a, uint32_t, int reps) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
-    hipLaunchKernelGGL((enc_slab_kernel<7, MODE, false>), dim3(blocks), dim3(640), 0, 0, a);
+    (void)launch_enc_mode<7, MODE, false>(a, 0);
     (void)hipEventRecord(e0, 0);
-    for (int r = 0; r < reps; r++) hipLaunchKernelGGL((enc_slab_kernel<7, MODE, false>), dim3(blocks), dim3(640), 0, 0, a);
+    for (int r = 0; r < reps; r++) (void)launch_enc_mode<7, MODE, false>(a, 0);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e0, e1);
+    if (hipGetLastError() != hipSuccess) printf("launch error\n");
     return ms / reps;
 }
 
@@ -28,7 +38,8 @@ int main(int argc, char **argv) {
     uint8_t *din, *dout;
     CK(hipMalloc(&din, nobj * L));
     CK(hipMalloc(&dout, nobj * 20 * slen));
-    CK(hipMemset(din, 0x5a, nobj * L));
+    if (argc > 2 && argv[2][0] == 'z') CK(hipMemset(din, 0x5a, nobj * L));
+    else hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, (uint32_t *)din, nobj * L / 4);
     std::vector<EncJob> jobs;
     for (int o = 0; o < nobj; o++)
         for (size_t s = 0; s < ns; s++) {
@@ -50,6 +61,12 @@ int main(int argc, char **argv) {
     const double alg = (double)nobj * (L + 20.0 * slen);
     const int reps = 5;
     float t;
+    if (argc > 3 && argv[3][0] == 'q') {  // quick: mode 0 only, best of 3
+        float best = 1e9f;
+        for (int i = 0; i < 3; i++) best = std::min(best, run<0>(a, blocks, reps));
+        printf("mode0 full (best of 3) %8.3f ms  %7.1f GB/s\n", best, alg / best / 1e6);
+        return 0;
+    }
     t = run<0>(a, blocks, reps); printf("mode0 full            %8.3f ms  %7.1f GB/s\n", t, alg / t / 1e6);
     t = run<1>(a, blocks, reps); printf("mode1 no-stores       %8.3f ms\n", t);
     t = run<2>(a, blocks, reps); printf("mode2 no-GF-math      %8.3f ms  %7.1f GB/s\n", t, alg / t / 1e6);

@@ -19,8 +19,10 @@ struct EncJob {
 struct EncArgs {
     const EncJob *jobs;
     uint32_t njobs;
-    uint32_t groups_per_stripe;  // ceil(words_per_stripe / 64): workgroups per stripe
+    uint32_t groups_per_stripe;  // ceil(words_per_stripe / 64): 64-word column groups per stripe
     uint32_t words_per_stripe;
+    uint32_t groups_per_wg;      // column groups one workgroup walks (all of them when they fit)
+    uint32_t wgs_per_stripe;     // ceil(groups_per_stripe / groups_per_wg)
     uint32_t cs;           // chunk size
     uint32_t sc;           // sub-chunk size
     uint32_t slice_len;
