@@ -6,6 +6,9 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 : > gpurun_out/kvar.log
+# warm-up (clocks / HBM training): one untimed pass of the first variant
+first=$(ls scripts/kbench_* | head -1)
+timeout -k 10 120 ./$first 1024 r q > /dev/null 2>&1 || exit $?
 for pass in 1 2; do
   for b in scripts/kbench_*; do
     echo "== $b (pass $pass)" >> gpurun_out/kvar.log

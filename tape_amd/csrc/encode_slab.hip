@@ -88,16 +88,24 @@ constexpr int kEncSlots = 25;
 #ifndef TEC_ENC_LOCKSTEP
 #define TEC_ENC_LOCKSTEP 0  // s_barrier every N planes (0: none): the workgroup's waves write rows together
 #endif
-constexpr uint32_t kEncMaxGroupsPerWg = 8;  // waves per workgroup (10 MB stripes: 56 groups)
+constexpr uint32_t kEncMaxGroupsPerWg = 8;  // column groups per workgroup (10 MB stripes: 56 groups)
+#ifndef TEC_ENC_STRIPES_PER_WG
+#define TEC_ENC_STRIPES_PER_WG 2  // 2 x 6 waves for 1 MB stripes: 3 waves on each SIMD
+#endif
+constexpr uint32_t kEncMaxWavesPerWg = 16;
 
-inline size_t enc_lds_bytes(uint32_t waves) { return (size_t)waves * kEncSlots * 64 * 4; }
+#ifndef TEC_ENC_DRIFT
+#define TEC_ENC_DRIFT 0  // >0: a wave starts plane t only when every wave of its workgroup has
+                         // finished plane t - DRIFT (LDS progress words, no s_barrier)
+#endif
+inline size_t enc_lds_bytes(uint32_t waves) { return (size_t)waves * kEncSlots * 64 * 4 + kEncMaxWavesPerWg * 4; }
 
 // MODE (ablation builds only, scripts/kbench.hip): bit0 = drop global stores, bit1 = replace
 // GF arithmetic by plain XOR, bit2 = skip the LDS slot table.  Production uses MODE 0.
 // MASKED: the stripe's data end is not dword aligned (only an object's last stripe, when its
 // length is not a multiple of 4): words are masked per lane instead of relying on the range check.
 template <int K, int MODE = 0, bool MASKED = false>
-__global__ void __launch_bounds__(kEncMaxGroupsPerWg * 64, TEC_ENC_WAVES_PER_EU) enc_slab_kernel(EncArgs a) {
+__global__ void __launch_bounds__(kEncMaxWavesPerWg * 64, TEC_ENC_WAVES_PER_EU) enc_slab_kernel(EncArgs a) {
     constexpr SlabConst<K> RC = make_slab_const<K>();
     constexpr int NP0 = kQ - K;  // column-0 parity nodes
     static_assert(NP0 == 0 || NP0 == 3, "fast encode covers k = 7 and k = 10");
@@ -106,10 +114,23 @@ __global__ void __launch_bounds__(kEncMaxGroupsPerWg * 64, TEC_ENC_WAVES_PER_EU)
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     const int lane = threadIdx.x & 63;
     uint32_t *const slots = lds + wv * (kEncSlots * 64) + lane;      // thread-private, stride 64
+    volatile uint32_t *const progress = lds + (blockDim.x >> 6) * (kEncSlots * 64);  // [wave]
+    if constexpr (TEC_ENC_DRIFT > 0) {
+        if (lane == 0) progress[wv] = 0;
+        __syncthreads();
+    }
     // workgroup = groups [gb, gb + blockDim/64) of one stripe; every base address is uniform
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
-    const uint32_t job = tile / a.wgs_per_stripe;
-    const uint32_t g = (tile - job * a.wgs_per_stripe) * a.groups_per_wg + (uint32_t)wv;
+    const uint32_t sub = (uint32_t)wv / a.groups_per_wg, gl = (uint32_t)wv - sub * a.groups_per_wg;
+    uint32_t job, g;
+    if (a.stripes_per_wg > 1) {  // several whole stripes per workgroup (balanced over the SIMDs)
+        job = tile * a.stripes_per_wg + sub;
+        if (job >= a.njobs) job = a.njobs - 1;  // a short last workgroup redoes the last stripe
+        g = gl;
+    } else {
+        job = tile / a.wgs_per_stripe;
+        g = (tile - job * a.wgs_per_stripe) * a.groups_per_wg + gl;
+    }
     const EncJob J = a.jobs[job];
     const uint32_t cs = a.cs, sc = a.sc, slen = a.slice_len, wps = a.words_per_stripe;
     // Word of this lane (a wave past the last group redoes the stripe's last word).  When
@@ -323,6 +344,20 @@ __global__ void __launch_bounds__(kEncMaxGroupsPerWg * 64, TEC_ENC_WAVES_PER_EU)
             }
             if constexpr (TEC_ENC_LOCKSTEP > 0)
                 if ((z + 1) % TEC_ENC_LOCKSTEP == 0) __builtin_amdgcn_s_barrier();
+            if constexpr (TEC_ENC_DRIFT > 0) {
+                // publish "plane z done", then hold while any wave is DRIFT or more planes behind
+                if (lane == 0) progress[wv] = z + 1;
+                const uint32_t nw = blockDim.x >> 6;
+                if (z + 1 >= (uint32_t)TEC_ENC_DRIFT) {
+                    for (;;) {
+                        uint32_t mn = 0xffffffffu;
+                        for (uint32_t q = 0; q < nw; q++) mn = min(mn, progress[q]);
+                        mn = __builtin_amdgcn_readfirstlane(mn);
+                        if (mn + TEC_ENC_DRIFT >= z + 1) break;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+            }
         }
     }
 }
@@ -348,9 +383,15 @@ hipError_t launch_enc_mode(EncArgs a, hipStream_t s) {
     if (a.njobs == 0) return hipSuccess;
     a.groups_per_wg = a.groups_per_stripe < kEncMaxGroupsPerWg ? a.groups_per_stripe : kEncMaxGroupsPerWg;
     a.wgs_per_stripe = (a.groups_per_stripe + a.groups_per_wg - 1) / a.groups_per_wg;
-    const uint64_t blocks = (uint64_t)a.njobs * a.wgs_per_stripe;
+    a.stripes_per_wg = 1;
+    if (a.wgs_per_stripe == 1)
+        while (a.stripes_per_wg < TEC_ENC_STRIPES_PER_WG && (a.stripes_per_wg + 1) * a.groups_per_wg <= kEncMaxWavesPerWg)
+            a.stripes_per_wg++;
+    const uint64_t blocks = a.stripes_per_wg > 1 ? (a.njobs + a.stripes_per_wg - 1) / a.stripes_per_wg
+                                                 : (uint64_t)a.njobs * a.wgs_per_stripe;
+    const uint32_t waves = a.groups_per_wg * a.stripes_per_wg;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    const size_t lds = enc_lds_bytes(a.groups_per_wg);
+    const size_t lds = enc_lds_bytes(waves);
     static size_t lds_set = 0;  // per instantiation: raise the dynamic-LDS cap once
     if (lds > lds_set) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(enc_slab_kernel<K, MODE, MASKED>),
@@ -358,7 +399,7 @@ hipError_t launch_enc_mode(EncArgs a, hipStream_t s) {
         if (e != hipSuccess) return e;
         lds_set = lds;
     }
-    hipLaunchKernelGGL((enc_slab_kernel<K, MODE, MASKED>), dim3((uint32_t)blocks), dim3(a.groups_per_wg * 64), lds,
+    hipLaunchKernelGGL((enc_slab_kernel<K, MODE, MASKED>), dim3((uint32_t)blocks), dim3(waves * 64), lds,
                        s, a);
     return hipGetLastError();
 }

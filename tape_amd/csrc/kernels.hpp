@@ -23,6 +23,7 @@ struct EncArgs {
     uint32_t words_per_stripe;
     uint32_t groups_per_wg;      // column groups one workgroup walks (all of them when they fit)
     uint32_t wgs_per_stripe;     // ceil(groups_per_stripe / groups_per_wg)
+    uint32_t stripes_per_wg;     // whole stripes per workgroup when wgs_per_stripe == 1
     uint32_t cs;           // chunk size
     uint32_t sc;           // sub-chunk size
     uint32_t slice_len;
