@@ -125,11 +125,19 @@ __global__ void __launch_bounds__(kEncMaxWavesPerWg * 64, TEC_ENC_WAVES_PER_EU) 
     uint32_t job, g;
     if (a.stripes_per_wg > 1) {  // several whole stripes per workgroup (balanced over the SIMDs)
         job = tile * a.stripes_per_wg + sub;
-        if (job >= a.njobs) job = a.njobs - 1;  // a short last workgroup redoes the last stripe
         g = gl;
     } else {
         job = tile / a.wgs_per_stripe;
         g = (tile - job * a.wgs_per_stripe) * a.groups_per_wg + gl;
+    }
+    // Surplus waves (a short last workgroup, or groups past the stripe's last word) leave: a
+    // second wave on the same words would race with the values parked in the output (level 2).
+    // Lanes past the last word inside a live wave duplicate it in lockstep, which is benign.
+    if (job >= a.njobs || g * 64u >= a.words_per_stripe) {
+        if constexpr (TEC_ENC_DRIFT > 0) {
+            if (lane == 0) progress[wv] = 0xffffu;
+        }
+        return;
     }
     const EncJob J = a.jobs[job];
     const uint32_t cs = a.cs, sc = a.sc, slen = a.slice_len, wps = a.words_per_stripe;
