@@ -1,7 +1,7 @@
-// kbench.hip -- ablation microbenchmark of the encode kernel (not part of the product build).
-// Builds enc_slab_kernel<7, MODE> variants over a device-resident 1024 x 4 MiB batch and
+// kbench.hip -- microbenchmark of the encode kernel (not part of the product build).
+// Times enc_stage_kernel<7> over a device-resident 1024 x 4 MiB batch and
 // times each with hipEvents.  hipcc --offload-arch=gfx950 -O3 -std=c++20 -I tape_amd/csrc
-#include "../tape_amd/csrc/encode_slab.hip"
+#include "../tape_amd/csrc/encode_stage.hip"
 #include <cstdio>
 #include <vector>
 using namespace tec;
@@ -21,9 +21,9 @@ template <int MODE>
 float run(const EncArgs &a, uint32_t, int reps) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
-    (void)launch_enc_mode<7, MODE, false>(a, 0);
+    if (launch_stage<7, false>(a, 0) != hipSuccess) printf("launch failed\n");
     (void)hipEventRecord(e0, 0);
-    for (int r = 0; r < reps; r++) (void)launch_enc_mode<7, MODE, false>(a, 0);
+    for (int r = 0; r < reps; r++) (void)launch_stage<7, false>(a, 0);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms = 0;
@@ -57,6 +57,7 @@ int main(int argc, char **argv) {
     EncArgs a{};
     a.jobs = dj; a.njobs = (uint32_t)jobs.size(); a.words_per_stripe = (sc + 3) / 4;
     a.groups_per_stripe = (a.words_per_stripe + 63) / 64; a.cs = cs; a.sc = sc; a.slice_len = slen; a.n = 20;
+    CK(hipMalloc(&a.scratch, encode_rows_scratch_bytes(a)));
     const uint32_t blocks = a.njobs * a.groups_per_stripe;
     const double alg = (double)nobj * (L + 20.0 * slen);
     const int reps = 5;
@@ -68,11 +69,5 @@ int main(int argc, char **argv) {
         return 0;
     }
     t = run<0>(a, blocks, reps); printf("mode0 full            %8.3f ms  %7.1f GB/s\n", t, alg / t / 1e6);
-    t = run<1>(a, blocks, reps); printf("mode1 no-stores       %8.3f ms\n", t);
-    t = run<2>(a, blocks, reps); printf("mode2 no-GF-math      %8.3f ms  %7.1f GB/s\n", t, alg / t / 1e6);
-    t = run<4>(a, blocks, reps); printf("mode4 no-LDS-exchange %8.3f ms  %7.1f GB/s\n", t, alg / t / 1e6);
-    t = run<6>(a, blocks, reps); printf("mode6 no-GF no-LDS    %8.3f ms  %7.1f GB/s\n", t, alg / t / 1e6);
-    t = run<3>(a, blocks, reps); printf("mode3 no-st no-GF     %8.3f ms\n", t);
-    t = run<7>(a, blocks, reps); printf("mode7 loads only      %8.3f ms\n", t);
     return 0;
 }

@@ -106,6 +106,7 @@ struct Arena {
     std::vector<uint8_t> img, last;
     HostBuf stage;
     DevBuf dev;
+    DevBuf scratch;  // kernel workspace (encode level-2 parking), ordered like `dev`
     hipEvent_t ev = nullptr;
     bool ev_pending = false;
     hipStream_t last_stream = nullptr;
@@ -146,8 +147,20 @@ struct Arena {
         return TE_OK;
     }
     template <class T> const T *at(size_t off) const { return reinterpret_cast<const T *>(dev.as<uint8_t>() + off); }
+    // workspace of at least `bytes` for launches about to be enqueued on stream s
+    int workspace(size_t bytes, hipStream_t s, uint8_t **out) {
+        if (bytes > scratch.cap) {
+            if (done_pending) TE_HIP(hipEventSynchronize(done));  // queued kernels may still use it
+            TE_HIP(scratch.ensure(bytes));
+        } else if (done_pending && last_stream != s) {
+            TE_HIP(hipStreamWaitEvent(s, done, 0));
+        }
+        *out = scratch.as<uint8_t>();
+        return TE_OK;
+    }
     void release() {
         dev.release();
+        scratch.release();
         stage.release();
         if (ev) (void)hipEventDestroy(ev);
         if (done) (void)hipEventDestroy(done);
@@ -474,13 +487,29 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
         for (int i = 0; i < 16; i++) a.qpow[i] = h.qpow[i];
         return a;
     };
+    // one workspace for every fast-path launch of the call (they run in stream order)
+    auto fast_path = [&](const Launch &L) { return c->fast_encode && (uint64_t)n * L.key.slice_len < 0x7fffffffull; };
+    size_t scratch_bytes = 0;
+    for (const Launch &L : launches) {
+        if (!fast_path(L)) continue;
+        const uint32_t wps = ((uint32_t)(L.key.cs / h.alpha) + 3) / 4;
+        EncArgs a{};
+        a.njobs = (uint32_t)L.count;
+        a.groups_per_stripe = (wps + 63) / 64;
+        scratch_bytes = std::max(scratch_bytes, encode_rows_scratch_bytes(a));
+    }
+    uint8_t *scratch = nullptr;
+    if (scratch_bytes) {
+        r = A.workspace(scratch_bytes, s, &scratch);
+        if (r) return r;
+    }
     size_t gi = 0;
     for (const Launch &L : launches) {
         const uint32_t cs = (uint32_t)L.key.cs, sc = cs / (uint32_t)h.alpha;
         const uint32_t wps = (sc + 3) / 4;   // words incl. a 2-column tail when sc % 4 == 2
         const uint32_t full = sc / 4;        // full 4-column words
         // fast kernel addresses an object's slices with 31-bit buffer offsets
-        if (c->fast_encode && (uint64_t)n * L.key.slice_len < 0x7fffffffull) {
+        if (fast_path(L)) {
             (void)full;
             EncArgs a{};
             a.jobs = A.at<EncJob>(L.off);
@@ -491,6 +520,7 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
             a.sc = sc;
             a.slice_len = (uint32_t)L.key.slice_len;
             a.n = (uint32_t)n;
+            a.scratch = scratch;
             TE_HIP(launch_encode_rows(h.k, L.key.masked, a, s));
         } else {
             TE_HIP(launch_gpe(gpe_args(gi, L, 0, wps), (uint32_t)pat.nerased, s));

@@ -28,6 +28,7 @@ struct EncArgs {
     uint32_t sc;           // sub-chunk size
     uint32_t slice_len;
     uint32_t n;
+    uint8_t *scratch;      // level-2 parking, encode_rows_scratch_bytes() bytes
 };
 
 // Metadata suffix writer: one 48-byte record per object, copied to its n slices.
@@ -116,5 +117,6 @@ hipError_t launch_meta(const MetaJob *jobs, uint32_t njobs, uint32_t n, hipStrea
 hipError_t launch_gpe(const GpeArgs &a, uint32_t max_erased, hipStream_t s);
 hipError_t launch_repair(const RepArgs &a, uint32_t max_erased, hipStream_t s);
 bool encode_rows_supported(int n, int k, int d);
+size_t encode_rows_scratch_bytes(const EncArgs &a);  // a.njobs, a.groups_per_stripe set
 
 }  // namespace tec
