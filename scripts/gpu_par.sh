@@ -7,5 +7,5 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 120 ./scripts/kbench 1024 r q > gpurun_out/kbench.log 2>&1 || exit $?
-for v in 1 2 3 4 8 12 15; do echo "ablate $v" >> gpurun_out/kbench.log; timeout -k 10 120 ./scripts/kbench_ab$v 1024 r q >> gpurun_out/kbench.log 2>&1 || exit $?; done
+for v in 1 2 3; do echo "ablate $v" >> gpurun_out/kbench.log; timeout -k 10 120 ./scripts/kbench_ab$v 1024 r q >> gpurun_out/kbench.log 2>&1 || exit $?; done
 exit $rc

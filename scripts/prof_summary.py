@@ -28,7 +28,7 @@ for name in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2"):
         agg = {}
         for r in csv.DictReader(open(cf)):
             k = r.get("Kernel_Name", "")
-            if "enc_slab" not in k and "gpe_kernel" not in k and "repair_kernel" not in k:
+            if "enc_stage" not in k and "gpe_kernel" not in k and "repair_kernel" not in k:
                 continue
             key = (k[:60], r["Counter_Name"])
             a = agg.setdefault(key, [0.0, 0])

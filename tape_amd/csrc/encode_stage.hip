@@ -175,6 +175,9 @@ struct Col1Holder {
 template <int G>
 __constant__ Col1Off<G> Col1Holder<G>::tab = make_col1_off<G>();
 
+#ifndef TEC_STAGE_PF
+#define TEC_STAGE_PF 1  // planes of load lookahead (1 or 2)
+#endif
 #ifndef TEC_STAGE_WAVES_PER_EU
 #define TEC_STAGE_WAVES_PER_EU 3
 #endif
@@ -321,13 +324,14 @@ __global__ void __launch_bounds__(G * 64, TEC_STAGE_WAVES_PER_EU) enc_stage_kern
     // Loads of plane (z0, s).  own[x] = C(x, (z0, s)) for the data nodes; part[x] = the
     // column-0 partner C(z0, (x, s)): an input chunk at level 1 (z0 < K); at level 2 a level-1
     // parity row re-read from HBM (x < K) or a U this lane parked in scratch (K <= x < z0).
-    uint32_t own[K], part[kQ];
-    auto load_own = [&](uint32_t z0, uint32_t s) {
+    uint32_t own[K], part[kQ];    // plane t + 1
+    uint32_t own2[K], part2[kQ];  // plane t + 2 (TEC_STAGE_PF == 2)
+    auto load_own_to = [&](uint32_t(&o)[K], uint32_t z0, uint32_t s) {
         const uint32_t so = src_al + (z0 * kQ + s) * sc;
 #pragma unroll
-        for (int x = 0; x < K; x++) own[x] = gload(rs_src, vo_own[x], so);
+        for (int x = 0; x < K; x++) o[x] = gload(rs_src, vo_own[x], so);
     };
-    auto load_part = [&](uint32_t z0, uint32_t s) {
+    auto load_part_to = [&](uint32_t(&part)[kQ], uint32_t z0, uint32_t s) {
         if (z0 < (uint32_t)K) {
             const uint32_t so = src_al + z0 * cs + s * sc;
 #pragma unroll
@@ -371,12 +375,20 @@ __global__ void __launch_bounds__(G * 64, TEC_STAGE_WAVES_PER_EU) enc_stage_kern
     // Branch-free row copy: every lane reads its LDS bytes unconditionally (past the row: junk
     // from the next row, or 0 past the allocation) and a lane with nothing to write stores at an
     // out-of-range offset, which the buffer range check drops.
+    // A row's last partial block (lseg % 16 bytes) is covered by one more lane storing the row's
+    // LAST 16 bytes (overlapping bytes rewritten with the same values; its LDS read is the only
+    // unaligned one) -- no separate narrow store per row.  Rows shorter than 16 bytes fall back
+    // to 16-bit stores.
     const uint32_t nb = lseg >> 4, tail = lseg & 15u;
     constexpr uint32_t kDrop = 0x80000000u;
-    const uint32_t vo0 = lane < nb ? lane * 16u : kDrop;
-    const uint32_t vo1 = lane + 64u < nb ? 1024u + lane * 16u : kDrop;
-    const uint32_t vot = lane < (tail >> 1) ? nb * 16u + lane * 2u : kDrop;
-    const uint32_t lt_off = nb * 16u + lane * 2u;  // tail LDS offset (in-row for lanes that store)
+    const bool wide_tail = tail != 0 && nb > 0;
+    auto blk_off = [&](uint32_t b) -> uint32_t {  // byte offset of lane block b, kDrop if none
+        return b < nb ? b * 16u : ((wide_tail && b == nb) ? lseg - 16u : kDrop);
+    };
+    const uint32_t vo0 = blk_off(lane), vo1 = blk_off(lane + 64u);
+    const uint32_t lo0 = vo0 == kDrop ? 0u : vo0, lo1 = vo1 == kDrop ? 0u : vo1;  // LDS offsets
+    const uint32_t vot = (!wide_tail && lane < (tail >> 1)) ? nb * 16u + lane * 2u : kDrop;
+    const uint32_t lt_off = nb * 16u + lane * 2u;  // 16-bit tail LDS offset (short rows only)
     auto item_off = [&](uint32_t it, uint32_t z0) -> uint32_t {
         const uint32_t node = (it >> 8) & 0xffu, tz0 = (it >> 16) & 0xffu, ts = it >> 24;
         const uint32_t plane = (tz0 == 0xffu ? z0 : tz0) * kQ + ts;
@@ -402,9 +414,9 @@ __global__ void __launch_bounds__(G * 64, TEC_STAGE_WAVES_PER_EU) enc_stage_kern
             for (int q = 0; q < CAP; q++) {
                 if ((uint32_t)q < n) {
                     const uint8_t *row = lds8 + (F.item[q] & 0xffu) * RS;
-                    d0[q] = rd128(row, lane * 16u);
-                    d1[q] = rd128(row, 1024u + lane * 16u);
-                    dt[q] = *reinterpret_cast<const uint16_t *>(row + lt_off);
+                    d0[q] = rd128(row, lo0);
+                    if (RS > 1024u) d1[q] = rd128(row, lo1);
+                    if (!wide_tail) dt[q] = *reinterpret_cast<const uint16_t *>(row + lt_off);
                 }
             }
             step_barrier();  // B1
@@ -414,16 +426,16 @@ __global__ void __launch_bounds__(G * 64, TEC_STAGE_WAVES_PER_EU) enc_stage_kern
                     const uint32_t off = item_off(F.item[q], z0);
                     st128(d0[q], vo0, off);
                     if (RS > 1024u) st128(d1[q], vo1, off);
-                    st16(dt[q], off);
+                    if (!wide_tail) st16(dt[q], off);
                 }
             }
         } else {  // small workgroups (short rows): row by row
             for (uint32_t q = 0; q < n; q++) {
                 const uint8_t *row = lds8 + (F.item[q] & 0xffu) * RS;
                 const uint32_t off = item_off(F.item[q], z0);
-                st128(rd128(row, lane * 16u), vo0, off);
-                if (RS > 1024u) st128(rd128(row, 1024u + lane * 16u), vo1, off);
-                st16(*reinterpret_cast<const uint16_t *>(row + lt_off), off);
+                st128(rd128(row, lo0), vo0, off);
+                if (RS > 1024u) st128(rd128(row, lo1), vo1, off);
+                if (!wide_tail) st16(*reinterpret_cast<const uint16_t *>(row + lt_off), off);
             }
             step_barrier();  // B1
         }
@@ -433,9 +445,16 @@ __global__ void __launch_bounds__(G * 64, TEC_STAGE_WAVES_PER_EU) enc_stage_kern
     // one is computed, except across the level-1 -> level-2 boundary, where the partners are
     // level-1 rows other waves stored: there every wave drains its stores (vmcnt(0)) and the
     // workgroup syncs first.
-    load_own(0, 0);
-    load_part(0, 0);
+    // With TEC_STAGE_PF == 2 the loads run two planes ahead; the partner loads of (K, 0) and
+    // (K, 1) then wait for the boundary drain.
+    load_own_to(own, 0, 0);
+    load_part_to(part, 0, 0);
+    if constexpr (TEC_STAGE_PF == 2) {
+        load_own_to(own2, 0, 1);
+        load_part_to(part2, 0, 1);
+    }
     for (uint32_t z0 = 0; z0 < (uint32_t)kQ; z0++) {
+#pragma unroll 2
         for (uint32_t s = 0; s < (uint32_t)kQ; s++) {
             const uint32_t z = z0 * kQ + s;
             uint32_t cown[K], cpart[kQ];
@@ -443,6 +462,12 @@ __global__ void __launch_bounds__(G * 64, TEC_STAGE_WAVES_PER_EU) enc_stage_kern
             for (int x = 0; x < K; x++) cown[x] = own[x];
 #pragma unroll
             for (int x = 0; x < kQ; x++) cpart[x] = part[x];
+            if constexpr (TEC_STAGE_PF == 2) {
+#pragma unroll
+                for (int x = 0; x < K; x++) own[x] = own2[x];
+#pragma unroll
+                for (int x = 0; x < kQ; x++) part[x] = part2[x];
+            }
             if (z == ez) {  // end-row substitution (see fixw)
 #pragma unroll
                 for (int x = 0; x < K; x++) cown[x] = (uint32_t)x == ex ? fixw : cown[x];
@@ -452,10 +477,17 @@ __global__ void __launch_bounds__(G * 64, TEC_STAGE_WAVES_PER_EU) enc_stage_kern
                 for (int x = 0; x < kQ; x++) cpart[x] = (uint32_t)x == ez / kQ ? fixw : cpart[x];
             }
             const bool boundary = NP0 > 0 && z0 + 1 == (uint32_t)K && s + 1 == (uint32_t)kQ;
-            if (z + 1 < (uint32_t)(kQ * kQ)) {
-                const uint32_t nz0 = s + 1 < (uint32_t)kQ ? z0 : z0 + 1, ns = s + 1 < (uint32_t)kQ ? s + 1 : 0;
-                load_own(nz0, ns);
-                if (!boundary) load_part(nz0, ns);
+            if (z + TEC_STAGE_PF < (uint32_t)(kQ * kQ)) {
+                const uint32_t t2 = z + TEC_STAGE_PF, nz0 = t2 / kQ, ns = t2 - nz0 * kQ;
+                // partners of level-2 planes are level-1 rows: only after the boundary drain
+                const bool after_drain = NP0 == 0 || nz0 < (uint32_t)K || z0 >= (uint32_t)K;
+                if constexpr (TEC_STAGE_PF == 2) {
+                    load_own_to(own2, nz0, ns);
+                    if (after_drain) load_part_to(part2, nz0, ns);
+                } else {
+                    load_own_to(own, nz0, ns);
+                    if (after_drain) load_part_to(part, nz0, ns);
+                }
             }
             if (z0 < (uint32_t)K) {
                 // ---- level 1: data partners are inputs; column-0 parity by type-1 recovery ----
@@ -475,7 +507,8 @@ __global__ void __launch_bounds__(G * 64, TEC_STAGE_WAVES_PER_EU) enc_stage_kern
                 if (boundary) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __syncthreads();
-                    load_part((uint32_t)K, 0);
+                    load_part_to(part, (uint32_t)K, 0);
+                    if constexpr (TEC_STAGE_PF == 2) load_part_to(part2, (uint32_t)K, 1);
                 }
             } else if constexpr (NP0 > 0) {
                 // ---- level 2: data partners are the level-1 column-0 parity C(z0, (x, s)) ----
