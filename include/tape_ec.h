@@ -63,6 +63,12 @@ int te_device_count(void);
 int te_set_device(int device);
 /* Detail of the last TE_ERR_HIP/OOM/NO_DEVICE on the calling thread (HIP error string). */
 const char *te_last_error_detail(void);
+/* Kernel timing (diagnostics for benchmarks): while enabled, every device batch call records a
+ * HIP event pair on its stream around its kernel launches (after descriptor upload).
+ * te_kernel_time_ms synchronises on the recorded events, returns their summed elapsed time and
+ * count, and clears them.  Off by default; no effect on results. */
+int te_kernel_timing(int enable);
+int te_kernel_time_ms(double *total_ms, uint32_t *count);
 /* Library build identification string. */
 const char *te_version(void);
 

@@ -96,6 +96,8 @@ def _load() -> C.CDLL:
         "te_device_count": (i, []),
         "te_set_device": (i, [i]),
         "te_version": (C.c_char_p, []),
+        "te_kernel_timing": (C.c_int, [C.c_int]),
+        "te_kernel_time_ms": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),
         "te_last_error_detail": (C.c_char_p, []),
         "te_clay_new": (i, [u32, u32, u32, C.POINTER(vp)]),
         "te_clay_from_params": (i, [u64, C.POINTER(vp)]),

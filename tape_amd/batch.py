@@ -18,11 +18,21 @@ def _stream_ptr(stream) -> C.c_void_p:
     return C.c_void_p(s.cuda_stream)
 
 
-def encode_batch(slicer: Slicer, data, objs: list[tuple[int, int, int, int]], out, stream=None) -> None:
-    """objs: (data_off, blob_len, out_off, chunk_index) per object; data/out are uint8 cuda tensors."""
-    arr = (_lib.te_object * len(objs))(*[_lib.te_object(*o) for o in objs])
+def _is_desc(objs) -> bool:
+    return hasattr(objs, "_length_")  # a prepared ctypes descriptor array
+
+
+def encode_descs(objs: list[tuple[int, int, int, int]]):
+    """Prepared te_object array for encode_batch / encode_batch_host (build once, reuse)."""
+    return (_lib.te_object * len(objs))(*[_lib.te_object(*o) for o in objs])
+
+
+def encode_batch(slicer: Slicer, data, objs, out, stream=None) -> None:
+    """objs: (data_off, blob_len, out_off, chunk_index) per object, or encode_descs(...) of them;
+    data/out are uint8 cuda tensors."""
+    arr = objs if _is_desc(objs) else encode_descs(objs)
     cfg = slicer._cfg()
-    r = lib.te_encode_batch_device(slicer.coder.handle, C.byref(cfg), C.c_void_p(data.data_ptr()), arr, len(objs),
+    r = lib.te_encode_batch_device(slicer.coder.handle, C.byref(cfg), C.c_void_p(data.data_ptr()), arr, len(arr),
                                    C.c_void_p(out.data_ptr()), _stream_ptr(stream))
     _check(r, "encode")
 
@@ -30,11 +40,23 @@ def encode_batch(slicer: Slicer, data, objs: list[tuple[int, int, int, int]], ou
 def encode_batch_host(slicer: Slicer, data, objs: list[tuple[int, int, int, int]], out, window_bytes: int = 0) -> None:
     """Host -> host batched encode (te_encode_batch_host): data/out are host buffers (numpy arrays
     or CPU tensors, pinned for full PCIe rate); objs as for encode_batch, offsets into data/out."""
-    arr = (_lib.te_object * len(objs))(*[_lib.te_object(*o) for o in objs])
+    arr = objs if _is_desc(objs) else encode_descs(objs)
     cfg = slicer._cfg()
-    r = lib.te_encode_batch_host(slicer.coder.handle, C.byref(cfg), C.c_void_p(_host_ptr(data)), arr, len(objs),
+    r = lib.te_encode_batch_host(slicer.coder.handle, C.byref(cfg), C.c_void_p(_host_ptr(data)), arr, len(arr),
                                  C.c_void_p(_host_ptr(out)), window_bytes)
     _check(r, "encode")
+
+
+def kernel_timing(enable: bool) -> None:
+    """te_kernel_timing: record HIP events around every batch call's kernel launches."""
+    _check(lib.te_kernel_timing(1 if enable else 0), "kernel timing")
+
+
+def kernel_time_ms() -> tuple[float, int]:
+    """(summed kernel ms, calls) since the last read (te_kernel_time_ms; synchronises)."""
+    ms, n = C.c_double(0), C.c_uint32(0)
+    _check(lib.te_kernel_time_ms(C.byref(ms), C.byref(n)), "kernel timing")
+    return ms.value, n.value
 
 
 def _host_ptr(buf) -> int:
@@ -44,20 +66,25 @@ def _host_ptr(buf) -> int:
     return buf.ctypes.data
 
 
-def decode_batch(slicer: Slicer, slices, objs: list[tuple[int, int, int, int]], metas: bytes, out,
-                 stream=None) -> None:
-    """objs: (slices_off, slice_len, avail_mask, out_off); metas: nobj*48 metadata bytes (host)."""
-    arr = (_lib.te_decode_object * len(objs))(*[_lib.te_decode_object(o[0], o[1], o[2], 0, o[3]) for o in objs])
+def decode_descs(objs: list[tuple[int, int, int, int]]):
+    """Prepared te_decode_object array for decode_batch (build once, reuse)."""
+    return (_lib.te_decode_object * len(objs))(*[_lib.te_decode_object(o[0], o[1], o[2], 0, o[3]) for o in objs])
+
+
+def decode_batch(slicer: Slicer, slices, objs, metas: bytes, out, stream=None) -> None:
+    """objs: (slices_off, slice_len, avail_mask, out_off), or decode_descs(...) of them; metas:
+    nobj*48 metadata bytes (host)."""
+    arr = objs if _is_desc(objs) else decode_descs(objs)
     cfg = slicer._cfg()
     mb = (C.c_uint8 * max(1, len(metas))).from_buffer_copy(metas if metas else b"\0")
     r = lib.te_decode_batch_device(slicer.coder.handle, C.byref(cfg), C.c_void_p(slices.data_ptr()), arr, mb,
-                                   len(objs), C.c_void_p(out.data_ptr()), _stream_ptr(stream))
+                                   len(arr), C.c_void_p(out.data_ptr()), _stream_ptr(stream))
     _check(r, "decode")
 
 
-def repair_batch(coder: ClayCoder, helpers, objs: list[tuple[RepairPlan, dict[int, int], int, bytes]], out,
-                 stream=None) -> None:
-    """objs: (plan, {helper_slice: offset in helpers tensor}, out_off, metadata48)."""
+def repair_descs(objs: list[tuple[RepairPlan, dict[int, int], int, bytes]]):
+    """Prepared te_repair_object array for repair_batch (build once, reuse; the plans must stay
+    alive while it is used)."""
     arr = (_lib.te_repair_object * len(objs))()
     for i, (plan, offs, out_off, meta) in enumerate(objs):
         arr[i].plan = plan.handle.value if hasattr(plan.handle, "value") else plan.handle
@@ -66,6 +93,13 @@ def repair_batch(coder: ClayCoder, helpers, objs: list[tuple[RepairPlan, dict[in
         arr[i].out_off = out_off
         for j, b in enumerate(meta):
             arr[i].metadata[j] = b
-    r = lib.te_repair_batch_device(coder.handle, C.c_void_p(helpers.data_ptr()), arr, len(objs),
+    return arr
+
+
+def repair_batch(coder: ClayCoder, helpers, objs, out, stream=None) -> None:
+    """objs: (plan, {helper_slice: offset in helpers tensor}, out_off, metadata48) per object, or
+    repair_descs(...) of them."""
+    arr = objs if _is_desc(objs) else repair_descs(objs)
+    r = lib.te_repair_batch_device(coder.handle, C.c_void_p(helpers.data_ptr()), arr, len(arr),
                                    C.c_void_p(out.data_ptr()), _stream_ptr(stream))
     _check(r, "repair")

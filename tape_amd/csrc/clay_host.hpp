@@ -166,6 +166,52 @@ struct ClayHost {
     }
 
     // Repair pattern (Ceph repair_one_lost_chunk): erased = lost column + aloof nodes.
+    // Uniform per-plane program of a repair pattern for the staged kernel (q = beta = kRepQ).
+    bool rep_prog(const RepPattern &P, const uint16_t *pool, const uint16_t *pind, RepProg &R) const {
+        if (q != kRepQ || (int)P.beta != kRepQ || t != 2) return false;
+        R = RepProg{};
+        const uint64_t amask = P.aloof_mask;
+        const int lost = (int)P.lost, xl = lost % q, yl = lost / q;
+        auto aidx = [&](int node) { return __builtin_popcountll(amask & ((1ull << node) - 1ull)); };
+        for (uint32_t e = 0; e < P.nerased; e++) {
+            const int node = P.erased[e], x = node % q;
+            R.enode[e] = (uint32_t)node;
+            if ((amask >> node) & 1ull) { R.ekind[e] = 0; R.erow[e] = (uint32_t)aidx(node); }
+            else if (node == lost) { R.ekind[e] = 1; R.erow[e] = 0; }
+            else { R.ekind[e] = x < xl ? 2 : 3; R.erow[e] = (uint32_t)(x < xl ? x + 1 : x); }
+        }
+        for (uint32_t j = 0; j < P.nknown; j++) R.knode0[j] = P.known[j];
+        const uint16_t *planes = pool + P.planes_off;
+        const uint32_t np = P.level_start[P.nlevels];
+        if (np != (uint32_t)kRepQ) return false;
+        for (uint32_t pi = 0; pi < np; pi++) {
+            RepProg::Step &S = R.step[pi];
+            const int z = planes[pi];
+            S.z = (uint32_t)z;
+            S.ri = pind[z];
+            for (uint32_t j = 0; j < P.nknown; j++) {
+                const int node = P.known[j], x = node % q, y = node / q, zy = digit(z, y);
+                if (zy == x) { S.kkind[j] = 0; continue; }
+                const int sw = y * q + zy;
+                const int zsw = z + (x - zy) * (int)qpow[t - 1 - y];
+                const int rsw = pind[zsw];
+                if ((amask >> sw) & 1ull) {
+                    S.kkind[j] = x > zy ? 4 : 3;
+                    S.krow[j] = (uint32_t)(aidx(sw) * kRepQ + rsw);
+                } else {
+                    S.kkind[j] = x > zy ? 2 : 1;
+                    S.knode[j] = (uint32_t)sw;
+                    S.krow[j] = (uint32_t)rsw;
+                }
+            }
+            for (int r = 0; r < kRepQ; r++) {
+                const int x = r == 0 ? xl : (r - 1 < xl ? r - 1 : r);
+                S.oplane[r] = (uint32_t)(z + (x - xl) * (int)qpow[t - 1 - yl]);
+            }
+        }
+        return true;
+    }
+
     bool rep_pattern(int lost_ext, const std::vector<int> &helpers_ext, RepPattern &P,
                      std::vector<uint16_t> &pool, std::vector<uint16_t> &pind) const {
         const int lost = ext_to_int(lost_ext);

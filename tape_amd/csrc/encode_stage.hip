@@ -175,6 +175,9 @@ struct Col1Holder {
 template <int G>
 __constant__ Col1Off<G> Col1Holder<G>::tab = make_col1_off<G>();
 
+#ifndef TEC_STAGE_ST_AUX
+#define TEC_STAGE_ST_AUX 0  // cache policy of the slice stores (gfx950: 2 = nt, 16 = sc1)
+#endif
 #ifndef TEC_STAGE_PF
 #define TEC_STAGE_PF 1  // planes of load lookahead (1 or 2)
 #endif
@@ -398,7 +401,7 @@ __global__ void __launch_bounds__(G * 64, TEC_STAGE_WAVES_PER_EU) enc_stage_kern
         if constexpr (TEC_STAGE_ABLATE & 1) {
             if (v.x == 0x12345678u) __builtin_amdgcn_raw_buffer_store_b32(v.y, rs_dst, (int)vo, (int)off, 0);
         } else {
-            __builtin_amdgcn_raw_buffer_store_b128(v, rs_dst, (int)vo, (int)off, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs_dst, (int)vo, (int)off, TEC_STAGE_ST_AUX);
         }
     };
     auto st16 = [&](uint32_t v, uint32_t off) {

@@ -168,6 +168,35 @@ struct Arena {
     }
 };
 
+// Kernel timing (te_kernel_timing): event pairs around each batch call's kernel launches.
+struct KTimeState {
+    std::mutex mu;
+    bool enabled = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pairs;
+} g_ktime;
+
+struct KTimer {
+    hipEvent_t a = nullptr, b = nullptr;
+    hipStream_t s;
+    explicit KTimer(hipStream_t st) : s(st) {
+        std::lock_guard<std::mutex> g(g_ktime.mu);
+        if (!g_ktime.enabled) return;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess || hipEventRecord(a, s) != hipSuccess) {
+            a = b = nullptr;
+        }
+    }
+    ~KTimer() {
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+    }
+    void stop() {
+        if (!a) return;
+        std::lock_guard<std::mutex> g(g_ktime.mu);
+        if (hipEventRecord(b, s) == hipSuccess) g_ktime.pairs.push_back({a, b});
+        a = b = nullptr;
+    }
+};
+
 void put_u64(uint8_t *p, uint64_t v) {
     for (int i = 0; i < 8; i++) p[i] = (uint8_t)(v >> (8 * i));
 }
@@ -244,6 +273,30 @@ int te_set_device(int device) {
 }
 
 const char *te_version(void) { return "tapeec 0.1.0 (gfx950)"; }
+
+int te_kernel_timing(int enable) {
+    std::lock_guard<std::mutex> g(g_ktime.mu);
+    g_ktime.enabled = enable != 0;
+    return TE_OK;
+}
+
+int te_kernel_time_ms(double *total_ms, uint32_t *count) {
+    if (!total_ms) return TE_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(g_ktime.mu);
+    double tot = 0;
+    for (auto &p : g_ktime.pairs) {
+        TE_HIP(hipEventSynchronize(p.second));
+        float ms = 0;
+        TE_HIP(hipEventElapsedTime(&ms, p.first, p.second));
+        tot += ms;
+        (void)hipEventDestroy(p.first);
+        (void)hipEventDestroy(p.second);
+    }
+    if (count) *count = (uint32_t)g_ktime.pairs.size();
+    g_ktime.pairs.clear();
+    *total_ms = tot;
+    return TE_OK;
+}
 
 // ------------------------------------------------------------------------------------------
 int te_clay_new(uint32_t n, uint32_t k, uint32_t d, te_clay **out) {
@@ -465,6 +518,23 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
     }
     int r = A.upload(s);
     if (r) return r;
+    // one workspace for every fast-path launch of the call (they run in stream order)
+    auto fast_path = [&](const Launch &L) { return c->fast_encode && (uint64_t)n * L.key.slice_len < 0x7fffffffull; };
+    size_t scratch_bytes = 0;
+    for (const Launch &L : launches) {
+        if (!fast_path(L)) continue;
+        const uint32_t wps = ((uint32_t)(L.key.cs / h.alpha) + 3) / 4;
+        EncArgs a{};
+        a.njobs = (uint32_t)L.count;
+        a.groups_per_stripe = (wps + 63) / 64;
+        scratch_bytes = std::max(scratch_bytes, encode_rows_scratch_bytes(a));
+    }
+    uint8_t *scratch = nullptr;
+    if (scratch_bytes) {
+        r = A.workspace(scratch_bytes, s, &scratch);
+        if (r) return r;
+    }
+    KTimer kt(s);
     if (!metas.empty()) TE_HIP(launch_meta(A.at<MetaJob>(meta_off), (uint32_t)metas.size(), (uint32_t)n, s));
     auto gpe_args = [&](size_t gi, const Launch &L, uint32_t word_base, uint32_t word_end) {
         const uint32_t cs = (uint32_t)L.key.cs, sc = cs / (uint32_t)h.alpha;
@@ -487,22 +557,6 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
         for (int i = 0; i < 16; i++) a.qpow[i] = h.qpow[i];
         return a;
     };
-    // one workspace for every fast-path launch of the call (they run in stream order)
-    auto fast_path = [&](const Launch &L) { return c->fast_encode && (uint64_t)n * L.key.slice_len < 0x7fffffffull; };
-    size_t scratch_bytes = 0;
-    for (const Launch &L : launches) {
-        if (!fast_path(L)) continue;
-        const uint32_t wps = ((uint32_t)(L.key.cs / h.alpha) + 3) / 4;
-        EncArgs a{};
-        a.njobs = (uint32_t)L.count;
-        a.groups_per_stripe = (wps + 63) / 64;
-        scratch_bytes = std::max(scratch_bytes, encode_rows_scratch_bytes(a));
-    }
-    uint8_t *scratch = nullptr;
-    if (scratch_bytes) {
-        r = A.workspace(scratch_bytes, s, &scratch);
-        if (r) return r;
-    }
     size_t gi = 0;
     for (const Launch &L : launches) {
         const uint32_t cs = (uint32_t)L.key.cs, sc = cs / (uint32_t)h.alpha;
@@ -527,6 +581,7 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
         }
         gi++;
     }
+    kt.stop();
     return A.mark_done(s);
 }
 
@@ -623,6 +678,7 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     for (auto &kv : groups) offs.push_back({kv.first, A.put(kv.second.data(), kv.second.size() * sizeof(GpeJob))});
     int r = A.upload(s);
     if (r) return r;
+    KTimer kt(s);
     for (auto &o : offs) {
         const uint64_t cs = o.first >> 32;
         const uint32_t sc = (uint32_t)(cs / (uint64_t)h.alpha);
@@ -644,6 +700,7 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         for (int i = 0; i < 16; i++) a.qpow[i] = h.qpow[i];
         TE_HIP(launch_gpe(a, max_er, s));
     }
+    kt.stop();
     return A.mark_done(s);
 }
 
@@ -708,9 +765,16 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
             metas.push_back(m);
         }
     }
+    // staged kernel when every pattern has a plane program
+    std::vector<RepProg> progs(pats.size());
+    bool staged = true;
+    for (size_t i = 0; i < pats.size() && staged; i++)
+        staged = repair_stage_supported(h.q, pats[i].beta, 8, pats[i].nerased, pats[i].nknown, pats[i].aloof_mask) &&
+                 h.rep_prog(pats[i], pool.data(), pind.data() + (size_t)i * h.alpha, progs[i]);
     Arena &A = c->rep;
     A.img.clear();
     const size_t pat_off = A.put(pats.data(), pats.size() * sizeof(RepPattern));
+    const size_t prog_off = staged ? A.put(progs.data(), progs.size() * sizeof(RepProg)) : 0;
     const size_t pool_off = A.put(pool.data(), pool.size() * sizeof(uint16_t));
     const size_t pind_off = A.put(pind.data(), pind.size() * sizeof(uint16_t));
     const size_t meta_off = A.put(metas.data(), metas.size() * sizeof(MetaJob));
@@ -718,6 +782,7 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
     for (auto &kv : groups) offs.push_back({kv.first, A.put(kv.second.data(), kv.second.size() * sizeof(RepJob))});
     int r = A.upload(s);
     if (r) return r;
+    KTimer kt(s);
     if (!metas.empty()) TE_HIP(launch_meta(A.at<MetaJob>(meta_off), (uint32_t)metas.size(), 1u, s));
     for (auto &o : offs) {
         const uint64_t cs = o.first;
@@ -733,8 +798,14 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
         a.groups_per_stripe = (wps + kGpeWords - 1) / kGpeWords;
         a.cs = (uint32_t)cs; a.sc = sc; a.q = h.q; a.t = h.t; a.alpha = h.alpha;
         for (int i = 0; i < 16; i++) a.qpow[i] = h.qpow[i];
-        TE_HIP(launch_repair(a, max_er, s));
+        if (staged && sc >= 8) {  // staged kernel: coalesced loads, whole-row stores
+            a.progs = A.at<RepProg>(prog_off);
+            TE_HIP(launch_repair_stage(a, s));
+        } else {
+            TE_HIP(launch_repair(a, max_er, s));
+        }
     }
+    kt.stop();
     return A.mark_done(s);
 }
 

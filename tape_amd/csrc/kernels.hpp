@@ -99,6 +99,23 @@ struct RepJob {
     uint32_t pad_;
 };
 
+// Staged repair kernel (repair_stage.hip): per pattern, the uniform control data of every
+// repair plane, host-resolved so the kernel does no index arithmetic (q = beta = 10 profiles).
+constexpr int kRepQ = 10;
+struct RepProg {                   // 32-bit fields: scalar loads have no sub-dword form on gfx950
+    uint32_t ekind[kGpeMaxErased];  // erased e: 0 aloof, 1 lost, 2 column-mate x < x_lost, 3 mate x > x_lost
+    uint32_t erow[kGpeMaxErased];   // aloof index (kind 0) / staging row (kinds 1-3)
+    uint32_t enode[kGpeMaxErased];  // erased node id
+    uint32_t knode0[kGpeMaxKnown];  // known node id
+    struct Step {
+        uint32_t z, ri;                   // plane, its repair row
+        uint32_t kkind[kGpeMaxKnown];     // known j: 0 red, 1/2 helper partner (x < / > z_y), 3/4 aloof partner
+        uint32_t knode[kGpeMaxKnown];     // partner node (kinds 1, 2)
+        uint32_t krow[kGpeMaxKnown];      // partner repair row (1, 2) or aloof LDS row ai * 10 + r (3, 4)
+        uint32_t oplane[kRepQ];           // staging row -> lost-chunk plane
+    } step[kRepQ];
+};
+
 struct RepArgs {
     const RepJob *jobs;
     const RepPattern *patterns;
@@ -107,6 +124,8 @@ struct RepArgs {
     uint32_t njobs, words_per_stripe, groups_per_stripe;
     uint32_t cs, sc, q, t, alpha;
     uint32_t qpow[16];
+    uint32_t wgs_per_stripe;          // staged kernel: workgroups per stripe row
+    const RepProg *progs;             // staged kernel: per pattern
 };
 
 constexpr int kGpeWords = 4;     // words (4 columns each) per GPE block
@@ -116,6 +135,8 @@ hipError_t launch_encode_rows(int k, bool masked, const EncArgs &a, hipStream_t 
 hipError_t launch_meta(const MetaJob *jobs, uint32_t njobs, uint32_t n, hipStream_t s);
 hipError_t launch_gpe(const GpeArgs &a, uint32_t max_erased, hipStream_t s);
 hipError_t launch_repair(const RepArgs &a, uint32_t max_erased, hipStream_t s);
+hipError_t launch_repair_stage(RepArgs a, hipStream_t s);
+bool repair_stage_supported(uint32_t q, uint32_t beta, uint32_t sc, uint32_t nerased, uint32_t nknown, uint64_t aloof_mask);
 bool encode_rows_supported(int n, int k, int d);
 size_t encode_rows_scratch_bytes(const EncArgs &a);  // a.njobs, a.groups_per_stripe set
 

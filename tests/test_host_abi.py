@@ -134,3 +134,14 @@ def test_extract_repair_data_matches_oracle(oracle):
             assert T.extract_repair_data(sl[h], p, h) == oracle.extract_repair_data(sl[h], cs, o.alpha, stripes, h)
         with pytest.raises(T.RepairError):
             T.extract_repair_data(sl[avail[0]][:100], p, avail[0])
+
+
+def test_kernel_timing_api_without_device():
+    """te_kernel_timing / te_kernel_time_ms are host bookkeeping: usable with no GPU, no events."""
+    import ctypes as C
+    from tape_amd._lib import lib
+    assert lib.te_kernel_timing(1) == 0
+    ms, n = C.c_double(-1), C.c_uint32(7)
+    assert lib.te_kernel_time_ms(C.byref(ms), C.byref(n)) == 0
+    assert ms.value == 0.0 and n.value == 0
+    assert lib.te_kernel_timing(0) == 0
