@@ -2,6 +2,10 @@
 // erasure-pattern tables the GPU engines consume.  Pure integer bookkeeping (the reference's
 // clay_codes::ClayCode::{new, minimum_to_repair} and the layered-decode ordering).
 #pragma once
+#include <algorithm>
+#include <map>
+#include <tuple>
+#include <vector>
 #include <stdint.h>
 #include <stddef.h>
 #include <vector>
@@ -128,6 +132,168 @@ struct ClayHost {
         for (int i = k + nu; cnt < m && i < qt; i++)
             if (!((mask >> i) & 1ull)) { mask |= 1ull << i; cnt++; }
         return mask;
+    }
+
+
+    // Staged-decode program (decode_stage.hip) for an erasure pattern: planes row by row along
+    // `orient` (0: rows = plane digit of column 0, 1: of column 1), within a row the planes whose
+    // inner digit is a known node first; every value a later plane needs gets a storage slot
+    // (lane-private LDS if consumed in the same row, per-stripe scratch otherwise).  Follows
+    // Ceph decode_layered (oracle/clay_oracle.c decode_layered) value by value; returns false
+    // when a dependency would be consumed before it is produced (then the generic engine runs).
+    bool dec_prog(const GpePattern &P, int orient, DecProgHdr &H, std::vector<DecStep> &out) const {
+        if (q != kRepQ || t != 2 || nu != 0 || alpha != kRepQ * kRepQ) return false;
+        if (P.nknown > (uint32_t)kDecMaxK || P.nerased > (uint32_t)kDecMaxE) return false;
+        const uint64_t em = P.erased_mask;
+        auto er = [&](int node) { return ((em >> node) & 1ull) != 0; };
+        auto isdata = [&](int node) { return node < k; };
+        const int yo = orient ? 1 : 0, yi = 1 - yo;
+        std::vector<int> rows, cols;
+        for (int pass = 0; pass < 2; pass++)
+            for (int r = 0; r < q; r++) {
+                if (er(yo * q + r) == (pass == 1)) rows.push_back(r);
+                if (er(yi * q + r) == (pass == 1)) cols.push_back(r);
+            }
+        std::vector<int> order, pos(alpha, -1);
+        for (int r : rows)
+            for (int c : cols) {
+                const int d0 = yo == 0 ? r : c, d1 = yo == 0 ? c : r;
+                pos[d0 * q + d1] = (int)order.size();
+                order.push_back(d0 * q + d1);
+            }
+        // values: (kind 0 = C / 1 = U, node, plane) -> producer / consumer step
+        struct Val { int prod = -1, cons = -1; uint32_t loc = kLocNone; };
+        std::map<std::tuple<int, int, int>, int> vid;
+        std::vector<Val> vals;
+        auto val = [&](int kind, int node, int z) {
+            auto key = std::make_tuple(kind, node, z);
+            auto f = vid.find(key);
+            if (f != vid.end()) return f->second;
+            vid[key] = (int)vals.size();
+            vals.push_back(Val{});
+            return (int)vals.size() - 1;
+        };
+        struct Ref { int val = -1; };  // value reference to patch with its location
+        out.assign(alpha, DecStep{});
+        std::vector<std::vector<std::pair<uint32_t *, int>>> patches(1);
+        auto &pl = patches[0];
+        uint32_t max_out = 0;
+        for (int st = 0; st < alpha; st++) {
+            const int z = order[st];
+            DecStep &S = out[st];
+            S.z = (uint32_t)z;
+            for (int i = 0; i < kDecMaxK; i++) S.kk[i] = kKnRed, S.kp[i] = 0, S.kout[i] = kLocNone;
+            for (int i = 0; i < kDecMaxE; i++) S.ek[i] = kErSkip, S.ep[i] = 0, S.ed0[i] = S.ed1[i] = S.epd[i] = kLocNone;
+            auto add_out = [&](int node, int plane) -> uint32_t {
+                if (S.nout >= (uint32_t)kDecMaxOut) return kLocNone;
+                S.out[S.nout] = (uint32_t)node | ((uint32_t)plane << 8);
+                return (kLocStage << 24) | S.nout++;
+            };
+            bool ok = true;
+            for (uint32_t j = 0; j < P.nknown; j++) {
+                const int N = P.known[j], x = N % q, y = N / q, zy = digit(z, y);
+                if (isdata(N)) { S.kout[j] = add_out(N, z); ok = ok && S.kout[j] != kLocNone; }
+                if (zy == x) { S.kk[j] = kKnRed; continue; }
+                const int M = y * q + zy, zsw = z + (x - zy) * (int)qpow[t - 1 - y];
+                if (!er(M)) {
+                    S.kk[j] = kKnInput;
+                    S.kp[j] = (uint32_t)M | ((uint32_t)zsw << 8);
+                } else {
+                    const int v = val(0, M, zsw);  // C of the erased partner, recovered earlier
+                    if (vals[v].cons >= 0) return false;
+                    vals[v].cons = st;
+                    S.kk[j] = kKnLoc;
+                    pl.push_back({&S.kp[j], v});
+                }
+            }
+            for (uint32_t e = 0; e < P.nerased; e++) {
+                const int N = P.erased[e], x = N % q, y = N / q, zy = digit(z, y);
+                if (zy == x) {  // red: C = U
+                    if (isdata(N)) { S.ek[e] = kErRed; S.ed0[e] = add_out(N, z); ok = ok && S.ed0[e] != kLocNone; }
+                    continue;
+                }
+                const int M = y * q + zy, zsw = z + (x - zy) * (int)qpow[t - 1 - y];
+                if (!er(M)) {  // type-1; the known partner consumes this C later
+                    S.ek[e] = kErType1;
+                    S.ep[e] = (uint32_t)M | ((uint32_t)zsw << 8);
+                    const int v = val(0, N, z);
+                    vals[v].prod = st;
+                    pl.push_back({&S.ed0[e], v});
+                    if (isdata(N)) { S.ed1[e] = add_out(N, z); ok = ok && S.ed1[e] != kLocNone; }
+                    continue;
+                }
+                if (!isdata(N) && !isdata(M)) continue;  // a parity pair nobody reads
+                if (pos[z] < pos[zsw]) {  // park this U for the pair's later plane
+                    S.ek[e] = kErPark;
+                    const int v = val(1, N, z);
+                    vals[v].prod = st;
+                    pl.push_back({&S.ep[e], v});
+                } else {  // finish the pair: both C's
+                    S.ek[e] = kErFinish;
+                    const int v = val(1, M, zsw);
+                    if (vals[v].prod < 0 || vals[v].cons >= 0) return false;
+                    vals[v].cons = st;
+                    pl.push_back({&S.ep[e], v});
+                    if (isdata(N)) { S.ed0[e] = add_out(N, z); ok = ok && S.ed0[e] != kLocNone; }
+                    if (isdata(M)) { S.epd[e] = add_out(M, zsw); ok = ok && S.epd[e] != kLocNone; }
+                }
+            }
+            if (!ok) return false;
+            max_out = std::max(max_out, S.nout);
+        }
+        // storage: lane-private LDS slot when producer and consumer share a row, scratch otherwise;
+        // interval colouring, a location reusable from its value's consumer step on
+        std::vector<int> idx(vals.size());
+        for (size_t i = 0; i < vals.size(); i++) {
+            if (vals[i].prod < 0 || vals[i].cons < 0 || vals[i].prod >= vals[i].cons) return false;
+            idx[i] = (int)i;
+        }
+        std::sort(idx.begin(), idx.end(), [&](int a, int b) { return vals[a].prod < vals[b].prod; });
+        std::vector<int> slot_free, scr_free;  // per location: first step it may be written again
+        for (int i : idx) {
+            Val &V = vals[i];
+            const bool same_row = V.prod / q == V.cons / q;
+            std::vector<int> &fl = same_row ? slot_free : scr_free;
+            size_t l = 0;
+            while (l < fl.size() && fl[l] > V.prod) l++;
+            if (l == fl.size()) fl.push_back(0);
+            fl[l] = V.cons;
+            V.loc = ((same_row ? kLocSlot : kLocScratch) << 24) | (uint32_t)l;
+        }
+        for (auto &p : pl) *p.first = vals[p.second].loc;
+        H = DecProgHdr{};
+        H.nsteps = (uint32_t)alpha;
+        H.nslots = (uint32_t)slot_free.size();
+        H.nscratch = (uint32_t)scr_free.size();
+        H.max_out = max_out;
+        for (uint32_t j = 0; j < P.nknown; j++) H.knode[j] = P.known[j];
+        return true;
+    }
+
+    // Packed step (DecStepP) of a dec_prog step; false when a location index needs > 8 bits.
+    static bool dec_pack(const DecStep &S, DecStepP &P) {
+        bool ok = true;
+        auto loc10 = [&](uint32_t loc) -> uint32_t {
+            if (loc == kLocNone) return kLoc10None;
+            const uint32_t ty = loc >> 24, ix = loc & 0xffffffu;
+            if (ix >= 256 || ty > kLocScratch) { ok = false; return kLoc10None; }
+            return ty << 8 | ix;
+        };
+        P = DecStepP{};
+        if (S.z >= 256 || S.nout > (uint32_t)kDecMaxOut) return false;
+        P.w[kDpHdr] = S.z | S.nout << 8;
+        for (int j = 0; j < kDecMaxK; j++) {
+            const uint32_t src = S.kk[j] == kKnLoc ? loc10(S.kp[j]) : (S.kk[j] == kKnInput ? S.kp[j] : 0u);
+            P.w[kDpKd + j] = S.kk[j] << 28 | loc10(S.kout[j]) << 16 | src;
+        }
+        for (int e = 0; e < kDecMaxE; e++) {
+            const uint32_t ek = S.ek[e];
+            const uint32_t src = ek == kErType1 ? S.ep[e] : ((ek == kErPark || ek == kErFinish) ? loc10(S.ep[e]) : 0u);
+            P.w[kDpEd + e] = ek << 28 | src;
+            P.w[kDpEo + e] = loc10(S.ed0[e]) | loc10(S.ed1[e]) << 10 | loc10(S.epd[e]) << 20;
+        }
+        for (uint32_t r = 0; r < S.nout; r++) P.w[kDpOut + r / 2] |= (S.out[r] & 0xffffu) << (16 * (r & 1));
+        return ok;
     }
 
     // Layered-decode pattern for the generic engine.  planes: appended to `pool`.

@@ -1,0 +1,315 @@
+// decode_stage.hip -- layered Clay decode for q = 10, t = 2 profiles (n = 20): ClayCoder::decode
+// (lib/slicer/src/clay.rs:106-122 -> clay_codes decode) inside Slicer::decode's per-stripe loop
+// (slicer.rs:333-361), any erasure pattern of at most n - k nodes.
+//
+// The host compiles each erasure pattern into a 100-step program (ClayHost::dec_prog): planes row
+// by row, and per plane which known node uncouples against what (an input row, or a C recovered
+// earlier), which erased U's the MDS solve must produce, and what becomes of them (a data row
+// written out, a type-1 C, or a pair's U parked for the pair's later plane).  The kernel follows it:
+//   * a workgroup owns one stripe's row segment (G <= 6 waves x 64 lanes x 4 columns); a lane
+//     owns one 4-column word of every plane, so every parked value is lane-private: an LDS slot
+//     when its consumer is in the same row, a per-stripe global scratch row otherwise;
+//   * loads are one dword per lane down each slice row (coalesced), one plane ahead; the MDS
+//     solve uses the pattern's decoding matrix as v_perm tables (scalar-loaded);
+//   * recovered and copied data rows are staged in LDS and written whole by one wave each.
+#include "kernels.hpp"
+#include "gf_dev.hpp"
+#include "dev_io.hpp"
+
+namespace tec {
+namespace dstage {
+
+constexpr int kMaxG = 6;
+constexpr uint32_t kMaxLdsRows = 56;  // staging + slots (G = 6: 86 KB)
+
+// PFT of the supported profiles: U = 3 C ^ 2 Cp = C ^ xt(C ^ Cp), and the inverse has the same
+// form (C = 3 U ^ 2 Up); type-1 C = t_u (U ^ Cp) ^ Cp.
+__device__ __forceinline__ uint32_t pft3(uint32_t a, uint32_t b) { return a ^ xt(a ^ b); }
+static_assert(kPft.u_c[0] == 3 && kPft.u_p[0] == 2 && kPft.c_u[0] == 3 && kPft.c_p[0] == 2 &&
+              kPft.u_c[1] == 3 && kPft.u_p[1] == 2 && kPft.c_u[1] == 3 && kPft.c_p[1] == 2, "PFT");
+static_assert(kPft.t_u[0] == kPft.t_u[1] && kPft.t_p[0] == kPft.t_p[1] && (kPft.t_u[0] ^ kPft.t_p[0]) == 1,
+              "type-1 C = t (U ^ Cp) ^ Cp");
+
+template <int NK, int G>
+__global__ void __launch_bounds__(G * 64, 2) dec_stage_kernel(DecArgs a) {
+    constexpr int NE = 2 * kRepQ - NK;  // padded patterns: every other node erased
+    constexpr uint32_t RS = G * 256u;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint8_t *const lds8 = reinterpret_cast<uint8_t *>(lds);
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t col_local = threadIdx.x * 4u;
+
+    const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
+    const uint32_t job = tile / a.wgs_per_stripe, seg = tile - job * a.wgs_per_stripe;
+    typedef const __attribute__((address_space(4))) GpeJob cJob;
+    typedef const __attribute__((address_space(4))) DecProgHdr cHdr;
+    typedef const __attribute__((address_space(4))) uint32_t cU32;
+    cJob &J = *(cJob *)(uintptr_t)(a.jobs + job);
+    cHdr &H = *(cHdr *)(uintptr_t)(a.hdrs + J.pattern);
+    const DecStepP *prog = a.steps + ((cU32 *)(uintptr_t)a.step_off)[J.pattern];
+    const uint32_t sc = a.sc, wps = a.words_per_stripe;
+    const uint32_t seg0 = seg * RS, lseg = min(RS, sc - seg0);
+    uint32_t w = seg * G * 64u + threadIdx.x;
+    if (w >= wps) w = wps - 1;
+    const uint32_t col = w * 4u;
+    // a word whose high half lies past the sub-chunk (sc = 2 mod 4) loads the dword 2 bytes
+    // earlier and rotates: the last row of the last slice may end the buffer
+    const bool tailw = col + 4u > sc;
+    const uint32_t vcol = tailw ? col - 2u : col, vsh = tailw ? 2u : 0u;
+    const uint32_t in_range = (uint32_t)(a.n * a.in_stride);  // host-checked < 2^31
+    const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc((void *)J.in, 0, (int)in_range, 0x00020000);
+    // data chunk x at out + x * out_stride, trimmed to the stripe's share of the object
+    const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc((void *)J.out, 0, (int)(uint32_t)J.out_len, 0x00020000);
+    uint8_t *const scr = a.scratch + (size_t)tile * a.nscratch_max * RS;
+    const __amdgpu_buffer_rsrc_t rs_scr = __builtin_amdgcn_make_buffer_rsrc(scr, 0, (int)(a.nscratch_max * RS), 0x00020000);
+    // input slice byte offset of internal node i (= shard i, nu = 0) in lane i, rotated
+    uint32_t sl_lane = lane + J.rot;
+    sl_lane = (sl_lane >= a.n ? sl_lane - a.n : sl_lane) * (uint32_t)a.in_stride;
+    auto in_off = [&](uint32_t src) -> uint32_t {  // src = node | plane << 8
+        return __builtin_amdgcn_readlane(sl_lane, src & 0xffu) + ((src >> 8) & 0xffu) * sc;
+    };
+    uint32_t kbase[NK];  // the known nodes' slices
+#pragma unroll
+    for (int j = 0; j < NK; j++) kbase[j] = __builtin_amdgcn_readlane(sl_lane, H.knode[j]);
+    auto ldin = [&](uint32_t so) -> uint32_t {
+        const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rs_in, (int)vcol, (int)so, 0);
+        return __builtin_amdgcn_alignbyte(v, v, vsh);
+    };
+    const uint32_t stage_rows = H.max_out;  // LDS rows [0, max_out) staging, then the slots
+    auto lds_at = [&](uint32_t row) -> uint32_t * { return reinterpret_cast<uint32_t *>(lds8 + row * RS + col_local); };
+    auto put = [&](uint32_t loc, uint32_t v) {  // 10-bit location: staging row / slot / scratch row
+        loc &= 0x3ffu;
+        if (loc == kLoc10None) return;
+        const uint32_t ty = loc >> 8, ix = loc & 0xffu;
+        if (ty == kLocStage) *lds_at(ix) = v;
+        else if (ty == kLocSlot) *lds_at(stage_rows + ix) = v;
+        else __builtin_amdgcn_raw_buffer_store_b32(v, rs_scr, (int)col_local, (int)(ix * RS), 0);
+    };
+    auto loc_ty = [](uint32_t src) { return (src >> 8) & 3u; };
+    auto get_slot = [&](uint32_t src) -> uint32_t { return *lds_at(stage_rows + (src & 0xffu)); };
+
+    // flush: staging row i -> data chunk x at the item's plane, the whole row by one wave
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint32_t nb = lseg >> 4, tail = lseg & 15u;
+    constexpr uint32_t kDrop = 0x80000000u;
+    const bool wide_tail = tail != 0 && nb > 0;
+    auto blk_off = [&](uint32_t b) -> uint32_t {
+        return b < nb ? b * 16u : ((wide_tail && b == nb) ? lseg - 16u : kDrop);
+    };
+    const uint32_t vo0 = blk_off(lane), vo1 = blk_off(lane + 64u);
+    const uint32_t lo0 = vo0 == kDrop ? 0u : vo0, lo1 = vo1 == kDrop ? 0u : vo1;
+    const uint32_t vot = (!wide_tail && lane < (tail >> 1)) ? nb * 16u + lane * 2u : kDrop;
+    const uint32_t lt_off = nb * 16u + lane * 2u;
+    // the stripe's output share ends at out_len, possibly inside a data row (the last chunk's
+    // padding, or the next stripe's share): a block across that end is written byte by byte
+    const uint32_t olen = (uint32_t)J.out_len;
+    auto flush16 = [&](const uint8_t *row, uint32_t lo, uint32_t vo, uint32_t off) {
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(row + lo);
+        if (vo == kDrop || off + vo + 16u <= olen) {
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs_out, (int)vo, (int)off, 0);
+        } else {
+#pragma unroll
+            for (uint32_t b = 0; b < 16u; b++)  // bytes past out_len fail the range check
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v[b >> 2] >> (8u * (b & 3u))), rs_out, (int)(vo + b), (int)off, 0);
+        }
+    };
+
+    // Control data in VGPRs, read out with v_readlane (scalar loads would serialise every step on
+    // lgkmcnt(0) waits): a step's 48 words in lanes 0..47 of one VGPR, loaded two steps ahead
+    // (vmcnt waits are in order), and the decoding matrix in the lanes of KDV VGPRs.
+    constexpr int kDW = NE * NK * 4, KDV = (kDW + 63) / 64;
+    uint32_t dv[KDV];
+    {
+        const uint32_t *dg = reinterpret_cast<const uint32_t *>(&a.patterns[J.pattern].D[0][0]);
+#pragma unroll
+        for (int i = 0; i < KDV; i++) {
+            const uint32_t idx = i * 64u + lane, e = idx / (NK * 4), j = (idx / 4) % NK, k = idx & 3u;
+            dv[i] = idx < (uint32_t)kDW ? dg[(e * kGpeMaxKnown + j) * 4 + k] : 0u;
+        }
+    }
+    auto dtab = [&](int e, int j, int k) -> uint32_t {
+        const int c = (e * NK + j) * 4 + k;
+        return __builtin_amdgcn_readlane(dv[c >> 6], c & 63);
+    };
+    const uint32_t *progw = prog[0].w + (lane < kDpWords ? lane : 0u);
+    auto ldw = [&](uint32_t st) -> uint32_t { return progw[st * kDpWords]; };
+    auto W = [](uint32_t v, int i) -> uint32_t { return __builtin_amdgcn_readlane(v, i); };
+    // input loads of a step: the known nodes' own rows, their input partners (uncoupling) and
+    // the type-1 partners; loads a step does not need read out of range (dropped, no traffic)
+    uint32_t own[NK], part[NK], tkp[NE];
+    auto load_step = [&](uint32_t wv_) {
+        const uint32_t z = W(wv_, kDpHdr) & 0xffu;
+#pragma unroll
+        for (int j = 0; j < NK; j++) {
+            own[j] = ldin(kbase[j] + z * sc);
+            const uint32_t kd = W(wv_, kDpKd + j);
+            part[j] = ldin((kd >> 28) == kKnInput ? in_off(kd) : kDrop);
+        }
+#pragma unroll
+        for (int e = 0; e < NE; e++) {
+            const uint32_t ed = W(wv_, kDpEd + e);
+            tkp[e] = ldin((ed >> 28) == kErType1 ? in_off(ed) : kDrop);
+        }
+    };
+    // scratch loads of a step, issued after the previous step's scratch stores (lane-private
+    // addresses: program order within the lane is the only ordering needed)
+    uint32_t ksc[NK], esc[NE];
+    auto scr_off = [&](uint32_t src) -> uint32_t { return (src & 0xffu) * RS; };
+    auto load_scr = [&](uint32_t wv_) {
+#pragma unroll
+        for (int j = 0; j < NK; j++) {
+            const uint32_t kd = W(wv_, kDpKd + j);
+            const bool on = (kd >> 28) == kKnLoc && loc_ty(kd) == kLocScratch;
+            ksc[j] = __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)col_local, (int)(on ? scr_off(kd) : kDrop), 0);
+        }
+#pragma unroll
+        for (int e = 0; e < NE; e++) {
+            const uint32_t ed = W(wv_, kDpEd + e);
+            const bool on = (ed >> 28) == kErFinish && loc_ty(ed) == kLocScratch;
+            esc[e] = __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)col_local, (int)(on ? scr_off(ed) : kDrop), 0);
+        }
+    };
+
+    const uint32_t nsteps = H.nsteps;
+    uint32_t w_cur = ldw(0), w_nxt = ldw(1);  // steps nsteps, nsteps + 1 are blank
+    load_step(w_cur);
+    load_scr(w_cur);
+    for (uint32_t st = 0; st < nsteps; st++) {
+        const uint32_t w_nn = ldw(st + 2);
+        uint32_t cown[NK], cpart[NK], ctkp[NE];
+#pragma unroll
+        for (int j = 0; j < NK; j++) cown[j] = own[j], cpart[j] = part[j];
+#pragma unroll
+        for (int e = 0; e < NE; e++) ctkp[e] = tkp[e];
+        load_step(w_nxt);  // blank step: every load dropped
+        // ---- uncouple the known nodes ----
+        Sel sel[NK];
+#pragma unroll
+        for (int j = 0; j < NK; j++) {
+            const uint32_t kd = W(w_cur, kDpKd + j), kk = kd >> 28;
+            uint32_t p = cpart[j];
+            if (kk == kKnLoc) p = loc_ty(kd) == kLocSlot ? get_slot(kd) : ksc[j];
+            sel[j] = Sel(kk == kKnRed ? cown[j] : pft3(cown[j], p));
+        }
+        // ---- MDS-solve the erased U's the program needs ----
+        uint32_t acc[NE];
+#pragma unroll
+        for (int e = 0; e < NE; e++) {
+            acc[e] = 0;
+            if ((W(w_cur, kDpEd + e) >> 28) == kErSkip) continue;
+#pragma unroll
+            for (int j = 0; j < NK; j++)
+                acc[e] ^= perm_mul(sel[j], dtab(e, j, 0), dtab(e, j, 1), dtab(e, j, 2), dtab(e, j, 3));
+        }
+        // pair partners' U parked in LDS slots (read before this step's writes: a location may
+        // be rewritten from its consumer step on)
+        uint32_t pu[NE];
+#pragma unroll
+        for (int e = 0; e < NE; e++) {
+            const uint32_t ed = W(w_cur, kDpEd + e);
+            pu[e] = ((ed >> 28) == kErFinish && loc_ty(ed) == kLocSlot) ? get_slot(ed) : esc[e];
+        }
+        lds_barrier();  // B1: the previous step's staging rows have been read out
+#pragma unroll
+        for (int j = 0; j < NK; j++) put(W(w_cur, kDpKd + j) >> 16, cown[j]);  // known data rows: copies
+#pragma unroll
+        for (int e = 0; e < NE; e++) {
+            const uint32_t ed = W(w_cur, kDpEd + e), eo = W(w_cur, kDpEo + e), ek = ed >> 28;
+            if (ek == kErRed) {
+                put(eo, acc[e]);
+            } else if (ek == kErType1) {
+                const uint32_t c = mulc(kPft.t_u[0], acc[e] ^ ctkp[e]) ^ ctkp[e];
+                put(eo, c);
+                put(eo >> 10, c);
+            } else if (ek == kErPark) {
+                put(ed, acc[e]);
+            } else if (ek == kErFinish) {
+                put(eo, pft3(acc[e], pu[e]));
+                put(eo >> 20, pft3(pu[e], acc[e]));
+            }
+        }
+        load_scr(w_nxt);
+        lds_barrier();  // B2: the step's rows are staged
+        const uint32_t no = W(w_cur, kDpHdr) >> 8;
+        const uint32_t r_beg = (wv * no) / G, r_end = ((wv + 1) * no) / G;
+        for (uint32_t r = r_beg; r < r_end; r++) {
+            const uint8_t *row = lds8 + r * RS;
+            const uint32_t it = (__builtin_amdgcn_readlane(w_cur, kDpOut + (r >> 1)) >> (16u * (r & 1u))) & 0xffffu;
+            const uint32_t off = (it & 0xffu) * (uint32_t)a.out_stride + (it >> 8) * sc + seg0;
+            flush16(row, lo0, vo0, off);
+            if (RS > 1024u) flush16(row, lo1, vo1, off);
+            if (!wide_tail) {
+                const uint16_t v = *reinterpret_cast<const uint16_t *>(row + lt_off);
+                if (vot == kDrop || off + vot + 2u <= olen) {
+                    __builtin_amdgcn_raw_buffer_store_b16(v, rs_out, (int)vot, (int)off, 0);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, rs_out, (int)vot, (int)off, 0);
+                }
+            }
+        }
+        w_cur = w_nxt;
+        w_nxt = w_nn;
+    }
+}
+
+}  // namespace dstage
+
+bool decode_stage_fits(uint32_t nslots, uint32_t max_out) { return nslots + max_out <= dstage::kMaxLdsRows; }
+bool decode_stage_k(int k) { return k >= 7 && k <= 10; }
+
+static uint32_t dec_stage_g(uint32_t words_per_stripe) {
+    const uint32_t groups = (words_per_stripe + 63) / 64;
+    return groups < (uint32_t)dstage::kMaxG ? groups : (uint32_t)dstage::kMaxG;
+}
+
+size_t decode_stage_scratch_bytes(const DecArgs &a) {
+    const uint32_t groups = (a.words_per_stripe + 63) / 64, g = dec_stage_g(a.words_per_stripe);
+    const uint32_t wgs = (groups + g - 1) / g;
+    return (size_t)a.njobs * wgs * (a.nscratch_max ? a.nscratch_max : 1) * g * 256u;
+}
+
+template <int NK, int G>
+static hipError_t launch_dec_g(const DecArgs &a, uint64_t blocks, hipStream_t s) {
+    const size_t lds = (size_t)a.lds_rows * G * 256u;
+    static size_t lds_set = 0;
+    if (lds > lds_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(dstage::dec_stage_kernel<NK, G>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        lds_set = lds;
+    }
+    hipLaunchKernelGGL((dstage::dec_stage_kernel<NK, G>), dim3((uint32_t)blocks), dim3(G * 64), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int NK>
+static hipError_t launch_dec_k(const DecArgs &a, uint32_t g, uint64_t blocks, hipStream_t s) {
+    switch (g) {
+        case 1: return launch_dec_g<NK, 1>(a, blocks, s);
+        case 2: return launch_dec_g<NK, 2>(a, blocks, s);
+        case 3: return launch_dec_g<NK, 3>(a, blocks, s);
+        case 4: return launch_dec_g<NK, 4>(a, blocks, s);
+        case 5: return launch_dec_g<NK, 5>(a, blocks, s);
+        default: return launch_dec_g<NK, 6>(a, blocks, s);
+    }
+}
+
+hipError_t launch_decode_stage(DecArgs a, hipStream_t s) {
+    if (a.njobs == 0) return hipSuccess;
+    if (a.lds_rows == 0 || a.lds_rows > dstage::kMaxLdsRows || a.sc < 8 || !a.scratch || a.n != 2u * kRepQ ||
+        !decode_stage_k((int)a.nk))
+        return hipErrorInvalidValue;
+    const uint32_t groups = (a.words_per_stripe + 63) / 64, g = dec_stage_g(a.words_per_stripe);
+    a.wgs_per_stripe = (groups + g - 1) / g;
+    const uint64_t blocks = (uint64_t)a.njobs * a.wgs_per_stripe;
+    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    switch (a.nk) {
+        case 7: return launch_dec_k<7>(a, g, blocks, s);
+        case 8: return launch_dec_k<8>(a, g, blocks, s);
+        case 9: return launch_dec_k<9>(a, g, blocks, s);
+        default: return launch_dec_k<10>(a, g, blocks, s);
+    }
+}
+
+}  // namespace tec

@@ -670,16 +670,95 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         }
     }
     if (groups.empty()) return TE_OK;
+    // staged kernel (decode_stage.hip) when every pattern compiles to a plane program; of the two
+    // row orientations the one with fewer scratch rows
+    std::vector<DecProgHdr> dhdrs(pats.size());
+    std::vector<DecStepP> dsteps;
+    std::vector<uint32_t> dstep_off(pats.size());
+    uint32_t lds_rows = 0, nscr_max = 0;
+    bool staged = true;
+    for (size_t i = 0; i < pats.size() && staged; i++) {
+        DecProgHdr best{};
+        std::vector<DecStep> best_steps;
+        bool found = false;
+        // the kernel is compiled per k, with every other node erased (padded patterns)
+        if (!decode_stage_k(h.k) || pats[i].nknown != (uint32_t)h.k || pats[i].nerased != (uint32_t)(n - h.k)) {
+            staged = false;
+            break;
+        }
+        for (int orient = 0; orient < 2; orient++) {
+            DecProgHdr H;
+            std::vector<DecStep> st;
+            if (!h.dec_prog(pats[i], orient, H, st) || !decode_stage_fits(H.nslots, H.max_out)) continue;
+            if (!found || H.nscratch < best.nscratch) { best = H; best_steps.swap(st); found = true; }
+        }
+        staged = found;
+        if (!found) break;
+        dhdrs[i] = best;
+        dstep_off[i] = (uint32_t)dsteps.size();
+        for (const DecStep &S : best_steps) {
+            dsteps.emplace_back();
+            staged = staged && ClayHost::dec_pack(S, dsteps.back());
+        }
+        dsteps.resize(dsteps.size() + 2);  // blank steps: the kernel reads two steps ahead
+        lds_rows = std::max(lds_rows, best.nslots + best.max_out);
+        nscr_max = std::max(nscr_max, best.nscratch);
+    }
+    lds_rows = std::max(lds_rows, 1u);
     Arena &A = c->dec;
     A.img.clear();
     const size_t pat_off = A.put(pats.data(), pats.size() * sizeof(GpePattern));
     const size_t pool_off = A.put(pool.data(), pool.size() * sizeof(uint16_t));
+    size_t hdr_off = 0, step_off = 0, soff_off = 0;
+    if (staged) {
+        hdr_off = A.put(dhdrs.data(), dhdrs.size() * sizeof(DecProgHdr));
+        step_off = A.put(dsteps.data(), dsteps.size() * sizeof(DecStepP), 64);
+        soff_off = A.put(dstep_off.data(), dstep_off.size() * sizeof(uint32_t));
+    }
     std::vector<std::pair<uint64_t, size_t>> offs;
     for (auto &kv : groups) offs.push_back({kv.first, A.put(kv.second.data(), kv.second.size() * sizeof(GpeJob))});
     int r = A.upload(s);
     if (r) return r;
+    // the staged kernel addresses a stripe's slices and its output share with 31-bit offsets
+    auto staged_group = [&](uint64_t key) {
+        const uint64_t cs = key >> 32, sc = cs / (uint64_t)h.alpha;
+        return staged && sc >= 8 && (uint64_t)n * group_in_stride[key] < 0x7fffffffull &&
+               cs * (uint64_t)h.k < 0x7fffffffull;
+    };
+    auto dec_args = [&](const std::pair<uint64_t, size_t> &o) {
+        const uint64_t cs = o.first >> 32;
+        const uint32_t sc = (uint32_t)(cs / (uint64_t)h.alpha);
+        DecArgs a{};
+        a.jobs = A.at<GpeJob>(o.second);
+        a.patterns = A.at<GpePattern>(pat_off);
+        a.hdrs = A.at<DecProgHdr>(hdr_off);
+        a.steps = A.at<DecStepP>(step_off);
+        a.step_off = A.at<uint32_t>(soff_off);
+        a.njobs = (uint32_t)groups[o.first].size();
+        a.words_per_stripe = (sc + 3) / 4;
+        a.cs = (uint32_t)cs; a.sc = sc; a.n = (uint32_t)n; a.nk = (uint32_t)h.k;
+        a.lds_rows = lds_rows;
+        a.nscratch_max = nscr_max;
+        a.in_stride = group_in_stride[o.first];
+        a.out_stride = cs;
+        return a;
+    };
+    size_t scratch_bytes = 0;
+    for (auto &o : offs)
+        if (staged_group(o.first)) scratch_bytes = std::max(scratch_bytes, decode_stage_scratch_bytes(dec_args(o)));
+    uint8_t *scratch = nullptr;
+    if (scratch_bytes) {
+        r = A.workspace(scratch_bytes, s, &scratch);
+        if (r) return r;
+    }
     KTimer kt(s);
     for (auto &o : offs) {
+        if (staged_group(o.first)) {
+            DecArgs a = dec_args(o);
+            a.scratch = scratch;
+            TE_HIP(launch_decode_stage(a, s));
+            continue;
+        }
         const uint64_t cs = o.first >> 32;
         const uint32_t sc = (uint32_t)(cs / (uint64_t)h.alpha);
         const uint32_t wps = sc >= 4 ? (sc + 3) / 4 : 1;

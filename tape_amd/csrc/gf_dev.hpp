@@ -49,6 +49,7 @@ struct Mult {
 
 struct Sel {
     uint32_t s0, s1, s2, s3;
+    __device__ __forceinline__ Sel() {}
     __device__ __forceinline__ explicit Sel(uint32_t x)
         : s0(x & 0x03030303u), s1((x >> 2) & 0x03030303u), s2((x >> 4) & 0x03030303u),
           s3((x >> 6) & 0x03030303u) {}

@@ -116,6 +116,45 @@ struct RepProg {                   // 32-bit fields: scalar loads have no sub-dw
     } step[kRepQ];
 };
 
+// Staged decode kernel (decode_stage.hip): a host-compiled program per erasure pattern for
+// q = 10, t = 2 profiles.  Planes run row by row (rows = one plane digit, "outer"); every value a
+// later plane needs is parked in a lane-private LDS slot (consumer in the same row) or in a
+// per-stripe global scratch row (later row).  Location codes: 0xffffffff none, else
+// type << 24 | index with type 0 staging row, 1 LDS slot, 2 scratch row.
+constexpr int kDecMaxK = 10, kDecMaxE = 13, kDecMaxOut = 16;
+constexpr uint32_t kLocNone = 0xffffffffu;
+enum : uint32_t { kLocStage = 0, kLocSlot = 1, kLocScratch = 2 };
+enum : uint32_t { kKnRed = 0, kKnInput = 1, kKnLoc = 2 };                       // known j kinds
+enum : uint32_t { kErSkip = 0, kErRed = 1, kErType1 = 2, kErPark = 3, kErFinish = 4 };  // erased e kinds
+struct DecStep {
+    uint32_t z;                    // plane
+    uint32_t nout;                 // flush items (item i = staging row i)
+    uint32_t out[kDecMaxOut];      // data chunk x | plane << 8
+    uint32_t kk[kDecMaxK];         // known j kind
+    uint32_t kp[kDecMaxK];         // kKnInput: partner node | plane << 8; kKnLoc: partner C location
+    uint32_t kout[kDecMaxK];       // staging row of the known node's C (data nodes), or none
+    uint32_t ek[kDecMaxE];         // erased e kind
+    uint32_t ep[kDecMaxE];         // type-1: partner node | plane << 8; park: U location; finish: partner U location
+    uint32_t ed0[kDecMaxE], ed1[kDecMaxE];  // destinations of C (red / type-1 / finish)
+    uint32_t epd[kDecMaxE];        // finish: destination of the partner's C
+};
+// The form the kernel reads (ClayHost::dec_pack): 48 dwords per step, lanes 0..47 of one VGPR.
+//   kd[j] = kind << 28 | kout << 16 | src        eo[e] = ed0 | ed1 << 10 | epd << 20
+//   ed[e] = kind << 28 | src                     out:  flush items, 16 bits each (x | plane << 8)
+//   src: node | plane << 8 (kKnInput, kErType1), else a 10-bit location;
+//   10-bit location: type << 8 | index, 0x3ff none.
+constexpr uint32_t kLoc10None = 0x3ffu;
+enum : uint32_t { kDpHdr = 0, kDpKd = 1, kDpEd = kDpKd + kDecMaxK, kDpEo = kDpEd + kDecMaxE,
+                  kDpOut = kDpEo + kDecMaxE, kDpWords = 48 };
+struct DecStepP {
+    uint32_t w[kDpWords];          // hdr = z | nout << 8
+};
+static_assert(kDpOut + kDecMaxOut / 2 <= kDpWords, "packed step");
+struct DecProgHdr {
+    uint32_t nsteps, nslots, nscratch, max_out;
+    uint32_t knode[kDecMaxK];      // known node ids (input slices)
+};
+
 struct RepArgs {
     const RepJob *jobs;
     const RepPattern *patterns;
@@ -130,6 +169,22 @@ struct RepArgs {
 
 constexpr int kGpeWords = 4;     // words (4 columns each) per GPE block
 constexpr int kGpePlaneThreads = 32;
+
+struct DecArgs {
+    const GpeJob *jobs;            // in = object's slice 0 + stripe*cs, out = object + stripe*S
+    const GpePattern *patterns;    // D tables
+    const DecProgHdr *hdrs;        // per pattern
+    const DecStepP *steps;         // per pattern: 100 steps + 2 blank, at step_off[pattern]
+    const uint32_t *step_off;
+    uint8_t *scratch;              // per workgroup tile: nscratch_max rows
+    uint32_t njobs, words_per_stripe, wgs_per_stripe;
+    uint32_t cs, sc, n, nk, lds_rows, nscratch_max;  // lds_rows: max over patterns of slots + staging rows
+    uint64_t in_stride, out_stride;
+};
+hipError_t launch_decode_stage(DecArgs a, hipStream_t s);
+size_t decode_stage_scratch_bytes(const DecArgs &a);
+bool decode_stage_fits(uint32_t nslots, uint32_t max_out);
+bool decode_stage_k(int k);  // a staged-decode kernel is compiled for this k (n = 20)
 
 hipError_t launch_encode_rows(int k, bool masked, const EncArgs &a, hipStream_t s);
 hipError_t launch_meta(const MetaJob *jobs, uint32_t njobs, uint32_t n, hipStream_t s);

@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(G * 64, 3) rep_stage_kernel(RepArgs a) {
     cPermTab(*D)[kGpeMaxKnown] = (cPermTab(*)[kGpeMaxKnown])(uintptr_t)(&PT.D[0][0]);
     for (uint32_t pi = 0; pi < (uint32_t)kQ; pi++) {
         const auto &S = PR.step[pi];
-        const uint32_t z = S.z, ri = S.ri;
+        const uint32_t ri = S.ri;
         // every load of the plane first: the known helpers' C, their helper partners' C, and the
         // column-mates' C
         uint32_t cv[MAXK], pv[MAXK], mcv[MAXE];

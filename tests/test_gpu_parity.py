@@ -131,6 +131,20 @@ def test_slicer_decode_patterns_4mib(oracle):
         assert s.decode([(i, sl[i]) for i in keep]) == data, keep
 
 
+@pytest.mark.parametrize("ln", [1, 999, 14_001, 100_003, 1_000_001])
+def test_slicer_decode_ragged_patterns(oracle, ln):
+    # staged decode: output shares ending inside a data row (ragged blobs, stripe < k * cs), every
+    # erasure count from 0 to n - k, both slice layouts
+    data = oracle.splitmix64_bytes(ln ^ 0x5EED, ln).tobytes()
+    rnd = random.Random(ln)
+    for rotated in (True, False):
+        s = T.Slicer.clay_default() if rotated else T.Slicer.new(T.ClayCoder(20, 7, 16))
+        sl = s.encode(data)
+        for ne in range(0, 14):
+            keep = sorted(rnd.sample(range(N), N - ne))
+            assert s.decode([(i, sl[i]) for i in keep]) == data, (rotated, keep)
+
+
 def test_slicer_layout_errors(oracle):
     s = T.Slicer.clay_default()
     sl = s.encode(oracle.test_pattern(2000))
