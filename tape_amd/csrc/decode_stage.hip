@@ -15,12 +15,17 @@
 #include "kernels.hpp"
 #include "gf_dev.hpp"
 #include "dev_io.hpp"
+#include <algorithm>
+#include <cstdlib>
 
 namespace tec {
 namespace dstage {
 
+#ifndef TEC_DEC_WPE
+#define TEC_DEC_WPE 4  // waves per SIMD the register budget is cut for
+#endif
 constexpr int kMaxG = 6;
-constexpr uint32_t kMaxLdsRows = 56;  // staging + slots (G = 6: 86 KB)
+constexpr uint32_t kMaxLdsRows = 64;  // 2 x staging + zero + trash + slots (G = 6: 96 KB)
 
 // PFT of the supported profiles: U = 3 C ^ 2 Cp = C ^ xt(C ^ Cp), and the inverse has the same
 // form (C = 3 U ^ 2 Up); type-1 C = t_u (U ^ Cp) ^ Cp.
@@ -31,7 +36,7 @@ static_assert(kPft.t_u[0] == kPft.t_u[1] && kPft.t_p[0] == kPft.t_p[1] && (kPft.
               "type-1 C = t (U ^ Cp) ^ Cp");
 
 template <int NK, int G>
-__global__ void __launch_bounds__(G * 64, 2) dec_stage_kernel(DecArgs a) {
+__global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs a) {
     constexpr int NE = 2 * kRepQ - NK;  // padded patterns: every other node erased
     constexpr uint32_t RS = G * 256u;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -76,19 +81,11 @@ __global__ void __launch_bounds__(G * 64, 2) dec_stage_kernel(DecArgs a) {
         const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rs_in, (int)vcol, (int)so, 0);
         return __builtin_amdgcn_alignbyte(v, v, vsh);
     };
-    const uint32_t stage_rows = H.max_out;  // LDS rows [0, max_out) staging, then the slots
-    auto lds_at = [&](uint32_t row) -> uint32_t * { return reinterpret_cast<uint32_t *>(lds8 + row * RS + col_local); };
-    auto put = [&](uint32_t loc, uint32_t v) {  // 10-bit location: staging row / slot / scratch row
-        loc &= 0x3ffu;
-        if (loc == kLoc10None) return;
-        const uint32_t ty = loc >> 8, ix = loc & 0xffu;
-        if (ty == kLocStage) *lds_at(ix) = v;
-        else if (ty == kLocSlot) *lds_at(stage_rows + ix) = v;
-        else __builtin_amdgcn_raw_buffer_store_b32(v, rs_scr, (int)col_local, (int)(ix * RS), 0);
-    };
-    auto loc_ty = [](uint32_t src) { return (src >> 8) & 3u; };
-    auto get_slot = [&](uint32_t src) -> uint32_t { return *lds_at(stage_rows + (src & 0xffu)); };
-
+    // LDS rows: two staging buffers of max_out rows (a step stages into buffer st & 1, so one
+    // barrier per step suffices), a zero row, a trash row, then the lane-private slots
+    const uint32_t mo = H.max_out, zrow = 2u * mo, trow = zrow + 1u, srow0 = zrow + 2u;
+    auto lds_at = [&](uint32_t off) -> uint32_t * { return reinterpret_cast<uint32_t *>(lds8 + off + col_local); };
+    *lds_at(zrow * RS) = 0u;  // lane-private: read back only by this lane
     // flush: staging row i -> data chunk x at the item's plane, the whole row by one wave
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t nb = lseg >> 4, tail = lseg & 15u;
@@ -97,14 +94,11 @@ __global__ void __launch_bounds__(G * 64, 2) dec_stage_kernel(DecArgs a) {
     auto blk_off = [&](uint32_t b) -> uint32_t {
         return b < nb ? b * 16u : ((wide_tail && b == nb) ? lseg - 16u : kDrop);
     };
-    const uint32_t vo0 = blk_off(lane), vo1 = blk_off(lane + 64u);
-    const uint32_t lo0 = vo0 == kDrop ? 0u : vo0, lo1 = vo1 == kDrop ? 0u : vo1;
-    const uint32_t vot = (!wide_tail && lane < (tail >> 1)) ? nb * 16u + lane * 2u : kDrop;
-    const uint32_t lt_off = nb * 16u + lane * 2u;
     // the stripe's output share ends at out_len, possibly inside a data row (the last chunk's
     // padding, or the next stripe's share): a block across that end is written byte by byte
     const uint32_t olen = (uint32_t)J.out_len;
-    auto flush16 = [&](const uint8_t *row, uint32_t lo, uint32_t vo, uint32_t off) {
+    auto flush16 = [&](const uint8_t *row, uint32_t b, uint32_t off) {  // block b of the row
+        const uint32_t vo = blk_off(b), lo = vo == kDrop ? 0u : vo;
         const u32x4 v = *reinterpret_cast<const u32x4 *>(row + lo);
         if (vo == kDrop || off + vo + 16u <= olen) {
             __builtin_amdgcn_raw_buffer_store_b128(v, rs_out, (int)vo, (int)off, 0);
@@ -115,60 +109,67 @@ __global__ void __launch_bounds__(G * 64, 2) dec_stage_kernel(DecArgs a) {
         }
     };
 
-    // Control data in VGPRs, read out with v_readlane (scalar loads would serialise every step on
-    // lgkmcnt(0) waits): a step's 48 words in lanes 0..47 of one VGPR, loaded two steps ahead
-    // (vmcnt waits are in order), and the decoding matrix in the lanes of KDV VGPRs.
-    constexpr int kDW = NE * NK * 4, KDV = (kDW + 63) / 64;
-    uint32_t dv[KDV];
-    {
-        const uint32_t *dg = reinterpret_cast<const uint32_t *>(&a.patterns[J.pattern].D[0][0]);
-#pragma unroll
-        for (int i = 0; i < KDV; i++) {
-            const uint32_t idx = i * 64u + lane, e = idx / (NK * 4), j = (idx / 4) % NK, k = idx & 3u;
-            dv[i] = idx < (uint32_t)kDW ? dg[(e * kGpeMaxKnown + j) * 4 + k] : 0u;
-        }
-    }
-    auto dtab = [&](int e, int j, int k) -> uint32_t {
-        const int c = (e * NK + j) * 4 + k;
-        return __builtin_amdgcn_readlane(dv[c >> 6], c & 63);
-    };
+    // Step control words in VGPRs: a step's 48 words in lanes 0..47 of one VGPR, loaded two
+    // steps ahead (vmcnt waits are in order).  Every per-word quantity (load offsets, LDS row
+    // offsets, scratch offsets) is derived for all words at once in vector code and read out with
+    // v_readlane, so the step needs no per-field scalar decoding or branches.  The decoding matrix
+    // (NE x NK v_perm tables, 1.5 KB per pattern) is scalar-loaded per erased row: its loads
+    // depend on nothing and stay in the scalar cache.
+    typedef const __attribute__((address_space(4))) PermTab cPermTab;
+    cPermTab(*D)[kGpeMaxKnown] = (cPermTab(*)[kGpeMaxKnown])(uintptr_t)(&a.patterns[J.pattern].D[0][0]);
     const uint32_t *progw = prog[0].w + (lane < kDpWords ? lane : 0u);
     auto ldw = [&](uint32_t st) -> uint32_t { return progw[st * kDpWords]; };
     auto W = [](uint32_t v, int i) -> uint32_t { return __builtin_amdgcn_readlane(v, i); };
-    // input loads of a step: the known nodes' own rows, their input partners (uncoupling) and
-    // the type-1 partners; loads a step does not need read out of range (dropped, no traffic)
+    const bool kd_l = lane >= kDpKd && lane < kDpKd + NK, ed_l = lane >= kDpEd && lane < kDpEd + NE;
+    const bool eo_l = lane >= kDpEo && lane < kDpEo + NE;
+    // input offset of the partner load word x describes (known input partner, type-1 partner)
+    auto vec_in = [&](uint32_t x) -> uint32_t {
+        const uint32_t k = x >> 28;
+        const bool on = (kd_l && k == kKnInput) || (ed_l && k == kErType1);
+        const uint32_t sl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((x & 0xffu) << 2), (int)sl_lane);
+        return on ? sl + ((x >> 8) & 0xffu) * sc : kDrop;
+    };
+    // a consumed location (known partner C, pair partner U): scratch offset or kDrop ...
+    auto consumed = [&](uint32_t x, uint32_t ty) {
+        const uint32_t k = x >> 28;
+        return ((kd_l && k == kKnLoc) || (ed_l && k == kErFinish)) && ((x >> 8) & 3u) == ty;
+    };
+    auto vec_scr = [&](uint32_t x) -> uint32_t { return consumed(x, kLocScratch) ? (x & 0xffu) * RS : kDrop; };
+    // ... and its LDS row (the zero row unless a slot)
+    auto vec_slot = [&](uint32_t x) -> uint32_t { return (consumed(x, kLocSlot) ? srow0 + (x & 0xffu) : zrow) * RS; };
+    // a produced value's 10-bit location -> LDS row offset (trash row for none / scratch)
+    auto dst_lds = [&](uint32_t f, uint32_t sbase) -> uint32_t {
+        const uint32_t ty = (f >> 8) & 3u, ix = f & 0xffu;
+        const uint32_t row = (f & 0x3ffu) == kLoc10None ? trow : ty == kLocStage ? sbase + ix : ty == kLocSlot ? srow0 + ix : trow;
+        return row * RS;
+    };
+    auto dst_scr = [&](uint32_t f) -> uint32_t {
+        return ((f & 0x3ffu) != kLoc10None && ((f >> 8) & 3u) == kLocScratch) ? (f & 0xffu) * RS : kDrop;
+    };
+
     uint32_t own[NK], part[NK], tkp[NE];
-    auto load_step = [&](uint32_t wv_) {
-        const uint32_t z = W(wv_, kDpHdr) & 0xffu;
+    auto load_step = [&](uint32_t x) {
+        const uint32_t zs = (W(x, kDpHdr) & 0xffu) * sc;
+        const uint32_t vin = vec_in(x);
 #pragma unroll
         for (int j = 0; j < NK; j++) {
-            own[j] = ldin(kbase[j] + z * sc);
-            const uint32_t kd = W(wv_, kDpKd + j);
-            part[j] = ldin((kd >> 28) == kKnInput ? in_off(kd) : kDrop);
+            own[j] = ldin(kbase[j] + zs);
+            part[j] = ldin(W(vin, kDpKd + j));
         }
 #pragma unroll
-        for (int e = 0; e < NE; e++) {
-            const uint32_t ed = W(wv_, kDpEd + e);
-            tkp[e] = ldin((ed >> 28) == kErType1 ? in_off(ed) : kDrop);
-        }
+        for (int e = 0; e < NE; e++) tkp[e] = ldin(W(vin, kDpEd + e));
     };
     // scratch loads of a step, issued after the previous step's scratch stores (lane-private
     // addresses: program order within the lane is the only ordering needed)
     uint32_t ksc[NK], esc[NE];
-    auto scr_off = [&](uint32_t src) -> uint32_t { return (src & 0xffu) * RS; };
-    auto load_scr = [&](uint32_t wv_) {
+    auto load_scr = [&](uint32_t x) {
+        const uint32_t vs = vec_scr(x);
 #pragma unroll
-        for (int j = 0; j < NK; j++) {
-            const uint32_t kd = W(wv_, kDpKd + j);
-            const bool on = (kd >> 28) == kKnLoc && loc_ty(kd) == kLocScratch;
-            ksc[j] = __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)col_local, (int)(on ? scr_off(kd) : kDrop), 0);
-        }
+        for (int j = 0; j < NK; j++)
+            ksc[j] = __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)col_local, (int)W(vs, kDpKd + j), 0);
 #pragma unroll
-        for (int e = 0; e < NE; e++) {
-            const uint32_t ed = W(wv_, kDpEd + e);
-            const bool on = (ed >> 28) == kErFinish && loc_ty(ed) == kLocScratch;
-            esc[e] = __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)col_local, (int)(on ? scr_off(ed) : kDrop), 0);
-        }
+        for (int e = 0; e < NE; e++)
+            esc[e] = __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)col_local, (int)W(vs, kDpEd + e), 0);
     };
 
     const uint32_t nsteps = H.nsteps;
@@ -182,16 +183,29 @@ __global__ void __launch_bounds__(G * 64, 2) dec_stage_kernel(DecArgs a) {
         for (int j = 0; j < NK; j++) cown[j] = own[j], cpart[j] = part[j];
 #pragma unroll
         for (int e = 0; e < NE; e++) ctkp[e] = tkp[e];
-        load_step(w_nxt);  // blank step: every load dropped
-        // ---- uncouple the known nodes ----
+        load_step(w_nxt);  // blank step: every partner load dropped
+        // ---- uncouple the known nodes: dropped loads read 0, a non-slot partner reads the zero
+        // row, a red node masks the PFT term ----
+        const uint32_t vsl = vec_slot(w_cur);
         Sel sel[NK];
 #pragma unroll
         for (int j = 0; j < NK; j++) {
-            const uint32_t kd = W(w_cur, kDpKd + j), kk = kd >> 28;
-            uint32_t p = cpart[j];
-            if (kk == kKnLoc) p = loc_ty(kd) == kLocSlot ? get_slot(kd) : ksc[j];
-            sel[j] = Sel(kk == kKnRed ? cown[j] : pft3(cown[j], p));
+            const uint32_t p = cpart[j] ^ ksc[j] ^ *lds_at(W(vsl, kDpKd + j));
+            const uint32_t mred = (W(w_cur, kDpKd + j) >> 28) == kKnRed ? 0u : ~0u;
+            sel[j] = Sel(cown[j] ^ (xt(cown[j] ^ p) & mred));
         }
+        // known data rows: copies (staging is double-buffered, so any time in the step)
+        const uint32_t sbase = (st & 1u) * mo;
+        {
+            const uint32_t lk = dst_lds(w_cur >> 16, sbase);
+#pragma unroll
+            for (int j = 0; j < NK; j++) *lds_at(W(lk, kDpKd + j)) = cown[j];
+        }
+        // pair partners' U (read before this step's writes: a location may be rewritten from its
+        // consumer step on)
+        uint32_t pu[NE];
+#pragma unroll
+        for (int e = 0; e < NE; e++) pu[e] = esc[e] ^ *lds_at(W(vsl, kDpEd + e));
         // ---- MDS-solve the erased U's the program needs ----
         uint32_t acc[NE];
 #pragma unroll
@@ -200,46 +214,46 @@ __global__ void __launch_bounds__(G * 64, 2) dec_stage_kernel(DecArgs a) {
             if ((W(w_cur, kDpEd + e) >> 28) == kErSkip) continue;
 #pragma unroll
             for (int j = 0; j < NK; j++)
-                acc[e] ^= perm_mul(sel[j], dtab(e, j, 0), dtab(e, j, 1), dtab(e, j, 2), dtab(e, j, 3));
+                acc[e] ^= perm_mul(sel[j], D[e][j].t[0], D[e][j].t[1], D[e][j].t[2], D[e][j].t[3]);
         }
-        // pair partners' U parked in LDS slots (read before this step's writes: a location may
-        // be rewritten from its consumer step on)
-        uint32_t pu[NE];
+        // ---- writes: lane A of a word is its general destination (known: kout; erased: the
+        // park location; eo: ed0), B and C the staging-only ed1 / epd ----
+        const uint32_t fa = kd_l ? (w_cur >> 16) : ed_l ? (((w_cur >> 28) == kErPark) ? w_cur : kLoc10None) : w_cur;
+        const uint32_t la = dst_lds(fa, sbase), sa = dst_scr(fa);
+        const uint32_t lb = dst_lds(w_cur >> 10, sbase), lc = dst_lds(w_cur >> 20, sbase);
+        auto put_a = [&](int i, uint32_t v) {
+            *lds_at(W(la, i)) = v;
+            const uint32_t so = W(sa, i);
+            if (so != kDrop) __builtin_amdgcn_raw_buffer_store_b32(v, rs_scr, (int)col_local, (int)so, 0);
+        };
 #pragma unroll
         for (int e = 0; e < NE; e++) {
-            const uint32_t ed = W(w_cur, kDpEd + e);
-            pu[e] = ((ed >> 28) == kErFinish && loc_ty(ed) == kLocSlot) ? get_slot(ed) : esc[e];
-        }
-        lds_barrier();  // B1: the previous step's staging rows have been read out
-#pragma unroll
-        for (int j = 0; j < NK; j++) put(W(w_cur, kDpKd + j) >> 16, cown[j]);  // known data rows: copies
-#pragma unroll
-        for (int e = 0; e < NE; e++) {
-            const uint32_t ed = W(w_cur, kDpEd + e), eo = W(w_cur, kDpEo + e), ek = ed >> 28;
+            const uint32_t ek = W(w_cur, kDpEd + e) >> 28;
             if (ek == kErRed) {
-                put(eo, acc[e]);
+                *lds_at(W(la, kDpEo + e)) = acc[e];
             } else if (ek == kErType1) {
                 const uint32_t c = mulc(kPft.t_u[0], acc[e] ^ ctkp[e]) ^ ctkp[e];
-                put(eo, c);
-                put(eo >> 10, c);
+                put_a(kDpEo + e, c);
+                *lds_at(W(lb, kDpEo + e)) = c;
             } else if (ek == kErPark) {
-                put(ed, acc[e]);
+                put_a(kDpEd + e, acc[e]);
             } else if (ek == kErFinish) {
-                put(eo, pft3(acc[e], pu[e]));
-                put(eo >> 20, pft3(pu[e], acc[e]));
+                *lds_at(W(la, kDpEo + e)) = pft3(acc[e], pu[e]);
+                *lds_at(W(lc, kDpEo + e)) = pft3(pu[e], acc[e]);
             }
         }
         load_scr(w_nxt);
-        lds_barrier();  // B2: the step's rows are staged
+        lds_barrier();  // the step's rows are staged (and the step before last's flushed)
         const uint32_t no = W(w_cur, kDpHdr) >> 8;
         const uint32_t r_beg = (wv * no) / G, r_end = ((wv + 1) * no) / G;
         for (uint32_t r = r_beg; r < r_end; r++) {
-            const uint8_t *row = lds8 + r * RS;
+            const uint8_t *row = lds8 + (sbase + r) * RS;
             const uint32_t it = (__builtin_amdgcn_readlane(w_cur, kDpOut + (r >> 1)) >> (16u * (r & 1u))) & 0xffffu;
             const uint32_t off = (it & 0xffu) * (uint32_t)a.out_stride + (it >> 8) * sc + seg0;
-            flush16(row, lo0, vo0, off);
-            if (RS > 1024u) flush16(row, lo1, vo1, off);
+            flush16(row, lane, off);
+            if (RS > 1024u) flush16(row, lane + 64u, off);
             if (!wide_tail) {
+                const uint32_t lt_off = nb * 16u + lane * 2u, vot = lane < (tail >> 1) ? lt_off : kDrop;
                 const uint16_t v = *reinterpret_cast<const uint16_t *>(row + lt_off);
                 if (vot == kDrop || off + vot + 2u <= olen) {
                     __builtin_amdgcn_raw_buffer_store_b16(v, rs_out, (int)vot, (int)off, 0);
@@ -255,7 +269,8 @@ __global__ void __launch_bounds__(G * 64, 2) dec_stage_kernel(DecArgs a) {
 
 }  // namespace dstage
 
-bool decode_stage_fits(uint32_t nslots, uint32_t max_out) { return nslots + max_out <= dstage::kMaxLdsRows; }
+uint32_t decode_stage_rows(uint32_t nslots, uint32_t max_out) { return 2 * max_out + 2 + nslots; }
+bool decode_stage_fits(uint32_t nslots, uint32_t max_out) { return decode_stage_rows(nslots, max_out) <= dstage::kMaxLdsRows; }
 bool decode_stage_k(int k) { return k >= 7 && k <= 10; }
 
 static uint32_t dec_stage_g(uint32_t words_per_stripe) {
@@ -304,6 +319,7 @@ hipError_t launch_decode_stage(DecArgs a, hipStream_t s) {
     a.wgs_per_stripe = (groups + g - 1) / g;
     const uint64_t blocks = (uint64_t)a.njobs * a.wgs_per_stripe;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    if (const char *x = getenv("TE_DEC_LDS_ROWS")) a.lds_rows = std::max<uint32_t>(a.lds_rows, std::min(atoi(x), 100));  // EXPERIMENT
     switch (a.nk) {
         case 7: return launch_dec_k<7>(a, g, blocks, s);
         case 8: return launch_dec_k<8>(a, g, blocks, s);

@@ -690,7 +690,12 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
             DecProgHdr H;
             std::vector<DecStep> st;
             if (!h.dec_prog(pats[i], orient, H, st) || !decode_stage_fits(H.nslots, H.max_out)) continue;
-            if (!found || H.nscratch < best.nscratch) { best = H; best_steps.swap(st); found = true; }
+            // rows for two workgroups per CU at 6 waves (2 x 53 x 1536 B <= 160 KB) first, then
+            // fewer scratch rows
+            auto cost = [](const DecProgHdr &x) {
+                return (decode_stage_rows(x.nslots, x.max_out) > 53 ? 1u << 20 : 0u) + x.nscratch;
+            };
+            if (!found || cost(H) < cost(best)) { best = H; best_steps.swap(st); found = true; }
         }
         staged = found;
         if (!found) break;
@@ -701,7 +706,7 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
             staged = staged && ClayHost::dec_pack(S, dsteps.back());
         }
         dsteps.resize(dsteps.size() + 2);  // blank steps: the kernel reads two steps ahead
-        lds_rows = std::max(lds_rows, best.nslots + best.max_out);
+        lds_rows = std::max(lds_rows, decode_stage_rows(best.nslots, best.max_out));
         nscr_max = std::max(nscr_max, best.nscratch);
     }
     lds_rows = std::max(lds_rows, 1u);

@@ -183,6 +183,7 @@ struct DecArgs {
 };
 hipError_t launch_decode_stage(DecArgs a, hipStream_t s);
 size_t decode_stage_scratch_bytes(const DecArgs &a);
+uint32_t decode_stage_rows(uint32_t nslots, uint32_t max_out);  // LDS rows of a program
 bool decode_stage_fits(uint32_t nslots, uint32_t max_out);
 bool decode_stage_k(int k);  // a staged-decode kernel is compiled for this k (n = 20)
 
