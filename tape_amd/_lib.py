@@ -11,7 +11,7 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtapeec.so")
+LIB_PATH = os.environ.get("TAPE_EC_LIB") or os.path.join(_HERE, "libtapeec.so")  # override: an alternate build
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "tape_ec.h")
 
 TE_OK = 0

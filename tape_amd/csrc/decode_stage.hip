@@ -15,12 +15,15 @@
 #include "kernels.hpp"
 #include "gf_dev.hpp"
 #include "dev_io.hpp"
-#include <algorithm>
-#include <cstdlib>
 
 namespace tec {
 namespace dstage {
 
+// measurement-only ablations (never in a shipped build): bit 0 no scratch loads, bit 1 no MDS
+// products, bit 2 no flush stores, bit 3 no input loads
+#ifndef TEC_DEC_ABLATE
+#define TEC_DEC_ABLATE 0
+#endif
 #ifndef TEC_DEC_WPE
 #define TEC_DEC_WPE 4  // waves per SIMD the register budget is cut for
 #endif
@@ -78,6 +81,7 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
 #pragma unroll
     for (int j = 0; j < NK; j++) kbase[j] = __builtin_amdgcn_readlane(sl_lane, H.knode[j]);
     auto ldin = [&](uint32_t so) -> uint32_t {
+        if (TEC_DEC_ABLATE & 8) return so;
         const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rs_in, (int)vcol, (int)so, 0);
         return __builtin_amdgcn_alignbyte(v, v, vsh);
     };
@@ -164,6 +168,11 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
     uint32_t ksc[NK], esc[NE];
     auto load_scr = [&](uint32_t x) {
         const uint32_t vs = vec_scr(x);
+        if (TEC_DEC_ABLATE & 1) {
+            for (int j = 0; j < NK; j++) ksc[j] = 0;
+            for (int e = 0; e < NE; e++) esc[e] = 0;
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < NK; j++)
             ksc[j] = __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)col_local, (int)W(vs, kDpKd + j), 0);
@@ -214,6 +223,7 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
             if ((W(w_cur, kDpEd + e) >> 28) == kErSkip) continue;
 #pragma unroll
             for (int j = 0; j < NK; j++)
+                if (TEC_DEC_ABLATE & 2) acc[e] ^= sel[j].s0 + e; else
                 acc[e] ^= perm_mul(sel[j], D[e][j].t[0], D[e][j].t[1], D[e][j].t[2], D[e][j].t[3]);
         }
         // ---- writes: lane A of a word is its general destination (known: kout; erased: the
@@ -246,7 +256,7 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
         lds_barrier();  // the step's rows are staged (and the step before last's flushed)
         const uint32_t no = W(w_cur, kDpHdr) >> 8;
         const uint32_t r_beg = (wv * no) / G, r_end = ((wv + 1) * no) / G;
-        for (uint32_t r = r_beg; r < r_end; r++) {
+        for (uint32_t r = r_beg; r < r_end && !(TEC_DEC_ABLATE & 4); r++) {
             const uint8_t *row = lds8 + (sbase + r) * RS;
             const uint32_t it = (__builtin_amdgcn_readlane(w_cur, kDpOut + (r >> 1)) >> (16u * (r & 1u))) & 0xffffu;
             const uint32_t off = (it & 0xffu) * (uint32_t)a.out_stride + (it >> 8) * sc + seg0;
@@ -319,7 +329,6 @@ hipError_t launch_decode_stage(DecArgs a, hipStream_t s) {
     a.wgs_per_stripe = (groups + g - 1) / g;
     const uint64_t blocks = (uint64_t)a.njobs * a.wgs_per_stripe;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    if (const char *x = getenv("TE_DEC_LDS_ROWS")) a.lds_rows = std::max<uint32_t>(a.lds_rows, std::min(atoi(x), 100));  // EXPERIMENT
     switch (a.nk) {
         case 7: return launch_dec_k<7>(a, g, blocks, s);
         case 8: return launch_dec_k<8>(a, g, blocks, s);

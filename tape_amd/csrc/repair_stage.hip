@@ -82,12 +82,12 @@ __global__ void __launch_bounds__(G * 64, 3) rep_stage_kernel(RepArgs a) {
     typedef const __attribute__((address_space(4))) PermTab cPermTab;
     cRepProg &PR = *(cRepProg *)(uintptr_t)(a.progs + J.pattern);
     cPermTab(*D)[kGpeMaxKnown] = (cPermTab(*)[kGpeMaxKnown])(uintptr_t)(&PT.D[0][0]);
-    for (uint32_t pi = 0; pi < (uint32_t)kQ; pi++) {
+    // every load of a plane: the known helpers' C, their helper partners' C and the column-mates'
+    // C; issued one plane ahead
+    uint32_t cv[MAXK], pv[MAXK], mcv[MAXE];
+    auto load_plane = [&](uint32_t pi) {
         const auto &S = PR.step[pi];
         const uint32_t ri = S.ri;
-        // every load of the plane first: the known helpers' C, their helper partners' C, and the
-        // column-mates' C
-        uint32_t cv[MAXK], pv[MAXK], mcv[MAXE];
 #pragma unroll
         for (int j = 0; j < MAXK; j++) {
             cv[j] = pv[j] = 0;
@@ -102,16 +102,27 @@ __global__ void __launch_bounds__(G * 64, 3) rep_stage_kernel(RepArgs a) {
             mcv[e] = 0;
             if ((uint32_t)e < ner && PR.ekind[e] >= 2) mcv[e] = load_h(PR.enode[e], ri);
         }
+    };
+    load_plane(0);
+    for (uint32_t pi = 0; pi < (uint32_t)kQ; pi++) {
+        const auto &S = PR.step[pi];
+        const uint32_t ri = S.ri;
+        uint32_t ccv[MAXK], cpv[MAXK], cmcv[MAXE];
+#pragma unroll
+        for (int j = 0; j < MAXK; j++) ccv[j] = cv[j], cpv[j] = pv[j];
+#pragma unroll
+        for (int e = 0; e < MAXE; e++) cmcv[e] = mcv[e];
+        if (pi + 1 < (uint32_t)kQ) load_plane(pi + 1);
         uint32_t acc[MAXE];
 #pragma unroll
         for (int e = 0; e < MAXE; e++) acc[e] = 0;
 #pragma unroll
         for (int j = 0; j < MAXK; j++) {
             if ((uint32_t)j >= nkn) continue;
-            const uint32_t c = cv[j], kk = S.kkind[j];
+            const uint32_t c = ccv[j], kk = S.kkind[j];
             uint32_t u = c;
-            if (kk == 1) u = mulc(kPft.u_c[0], c) ^ mulc(kPft.u_p[0], pv[j]);
-            if (kk == 2) u = mulc(kPft.u_c[1], c) ^ mulc(kPft.u_p[1], pv[j]);
+            if (kk == 1) u = mulc(kPft.u_c[0], c) ^ mulc(kPft.u_p[0], cpv[j]);
+            if (kk == 2) u = mulc(kPft.u_c[1], c) ^ mulc(kPft.u_p[1], cpv[j]);
             if (kk >= 3) {
                 const uint32_t pu = *reinterpret_cast<const uint32_t *>(lds8 + (kOutRows + S.krow[j]) * RS + col_local);
                 u = kk == 4 ? (mulc(kPft.a_c[1], c) ^ mulc(kPft.a_p[1], pu)) : (mulc(kPft.a_c[0], c) ^ mulc(kPft.a_p[0], pu));
@@ -132,8 +143,8 @@ __global__ void __launch_bounds__(G * 64, 3) rep_stage_kernel(RepArgs a) {
                 stage(0, acc[e]);  // the lost node is red in every repair plane: C = U
             } else {
                 // column-mate: its helper C and solved U give the lost node's C at the swapped plane
-                const uint32_t v = kind == 3 ? (mulc(kPft.l_c[1], mcv[e]) ^ mulc(kPft.l_u[1], acc[e]))
-                                             : (mulc(kPft.l_c[0], mcv[e]) ^ mulc(kPft.l_u[0], acc[e]));
+                const uint32_t v = kind == 3 ? (mulc(kPft.l_c[1], cmcv[e]) ^ mulc(kPft.l_u[1], acc[e]))
+                                             : (mulc(kPft.l_c[0], cmcv[e]) ^ mulc(kPft.l_u[0], acc[e]));
                 stage(row, v);
             }
         }
