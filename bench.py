@@ -7,7 +7,8 @@ profile Clay(20,7,16), rotated 1 MB stripes; one "step" = one te_encode_batch_de
 the whole batch (all 20 slices incl. metadata written to HBM).  Multi-GPU (torchrun): objects
 are partitioned across ranks (per-GPU batches, weak scaling), no data-path collective.
 
-Also: --mode repair (config 3) and --mode decode (config 4, slices 0..12 erased).
+Also: --mode repair (config 3), --mode decode (config 4, slices 0..12 erased) and --mode commit
+(hash_leaf of the 20 slices + merkle root + proofs of every encoded object).
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
@@ -29,6 +30,7 @@ ALG_BYTES = {  # algorithmic HBM bytes per 4 MiB object
     "encode": 4 * MiB + N * 715_048,
     "repair": 16 * 71_500 + 715_048,
     "decode": 7 * 715_048 + 4 * MiB,
+    "commit": N * 715_048 + N * 32 + 32 + N * 5 * 32,  # slices read; leaf hashes, root, proofs written
 }
 
 
@@ -97,7 +99,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--objects", type=int, default=1024, help="objects per GPU per step")
     ap.add_argument("--object-bytes", type=int, default=4 * MiB)
-    ap.add_argument("--mode", choices=["encode", "repair", "decode"], default="encode")
+    ap.add_argument("--mode", choices=["encode", "repair", "decode", "commit"], default="encode")
     ap.add_argument("--cpu-sample", type=int, default=96, help="objects in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity cores)")
     ap.add_argument("--copy-objects", type=int, default=256,
@@ -172,6 +174,15 @@ def main():
         def step():
             batch.repair_batch(slicer.coder, d_help, rep_objs, d_rep, stream)
 
+    elif args.mode == "commit":
+        from tape_amd import merkle
+        d_leaf = torch.empty(nobj * N * 32, dtype=torch.uint8, device=dev)
+        d_root = torch.empty(nobj * 32, dtype=torch.uint8, device=dev)
+        d_proof = torch.empty(nobj * N * T.SLICE_TREE_HEIGHT * 32, dtype=torch.uint8, device=dev)
+
+        def step():
+            merkle.commit_batch(d_out, per, g.slice_len, N, nobj, d_leaf, d_root, d_proof, T.SLICE_TREE_HEIGHT, stream)
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -207,6 +218,15 @@ def main():
         ref = torch.stack([d_out[i * per + (i % N) * sl:i * per + (i % N + 1) * sl] for i in range(nobj)])
         verified = bool(torch.equal(d_rep.view(nobj, sl), ref))
         del ref
+    elif args.mode == "commit":  # first and last object against hashlib (SHA-256 of "LEAF" || slice)
+        import hashlib
+        ok = True
+        for i in (0, nobj - 1):
+            lv = d_leaf[i * N * 32:(i + 1) * N * 32].cpu().numpy().tobytes()
+            for j in range(N):
+                sl = d_out[i * per + j * g.slice_len:i * per + (j + 1) * g.slice_len].cpu().numpy().tobytes()
+                ok = ok and lv[j * 32:(j + 1) * 32] == hashlib.sha256(b"LEAF" + sl).digest()
+        verified = ok
     copy_inc = None
     if args.mode == "encode" and args.copy_objects > 0:
         copy_inc = copy_inclusive(args, torch, dist, world, slicer, batch, d_in, d_out, per, L, dev)
@@ -214,6 +234,8 @@ def main():
     cpu = None
     if rank == 0 and args.cpu_sample > 0 and args.mode == "encode":
         cpu = cpu_baseline(args, np, torch, d_in, d_out, per, L)
+    if rank == 0 and args.cpu_sample > 0 and args.mode == "commit":
+        cpu = cpu_baseline_commit(args, d_out, per, g.slice_len, L)
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -224,7 +246,10 @@ def main():
             traffic = None
     if rank == 0:
         line = {
-            "metric": METRIC if args.mode == "encode" else f"device-resident {args.mode} GiB/s, batched 4 MiB objects, 1 MI355X",
+            "metric": METRIC if args.mode == "encode" else (
+                "device-resident slice-commitment GiB/s (hash_leaf x 20 + merkle root + proofs), batched 4 MiB "
+                "objects, 1 MI355X" if args.mode == "commit" else
+                f"device-resident {args.mode} GiB/s, batched 4 MiB objects, 1 MI355X"),
             "value": round(gib_s, 3),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -237,7 +262,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic (SplitMix64 per object, seed 0x7A9E5EED ^ id), device-resident",
             "config": {"workload": {"encode": "Slicer::encode", "repair": "Slicer::repair (lost = i mod 20)",
-                                    "decode": "Slicer::decode (slices 0..12 erased)"}[args.mode]
+                                    "decode": "Slicer::decode (slices 0..12 erased)",
+                                    "commit": "encode_with_proofs commitment (SHA-256 leaf per slice, height-5 root, 20 proofs)"}[args.mode]
                        + f" of {nobj} x {L} B objects per GPU, Clay(20,7,16) rotated, 1 MB stripes",
                        "objects_per_gpu": nobj, "object_bytes": L, "profile": "clay(20,7,16)",
                        "parallelism": f"objects partitioned over {world} GPU(s)"},
@@ -253,6 +279,24 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def cpu_baseline_commit(args, d_out, per, slice_len, L):
+    """CPU commitment of a bounded sample (the oracle: hashlib SHA-256, as the SDK's
+    solana-sha256-hasher would run it), one object per thread."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import merkle_oracle as O
+    ncpu = len(os.sched_getaffinity(0))
+    threads = args.cpu_threads or min(16, ncpu)
+    k = min(args.cpu_sample, d_out.numel() // per)
+    host = d_out[:k * per].cpu().numpy()
+    objs = [[host[i * per + j * slice_len:i * per + (j + 1) * slice_len].tobytes() for j in range(N)] for i in range(k)]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(O.commit_slices, objs))
+    dt = time.perf_counter() - t0
+    return {"value": round(k * L / dt / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{k} x 4 MiB objects' 20 slices, {threads} threads, one object per thread (hashlib SHA-256)"}
 
 
 def copy_inclusive(args, torch, dist, world, slicer, batch, d_in, d_out, per, L, dev):

@@ -47,6 +47,11 @@ typedef enum te_status {
     TE_ERR_INVALID_SLICE = 7,
     TE_ERR_CLAY = 8,
     TE_ERR_MISSING_HELPER = 9,
+    /* MerkleError (lib/crypto/src/merkle/tree.rs:360-366) */
+    TE_ERR_MERKLE_TREE_FULL = 10,
+    TE_ERR_MERKLE_INVALID_PROOF = 11,
+    TE_ERR_MERKLE_INVALID_INDEX = 12,
+    TE_ERR_MERKLE_PROOF_LENGTH = 13,
     /* engine */
     TE_ERR_INVALID_ARG = 20,
     TE_ERR_NO_DEVICE = 21,
@@ -227,6 +232,38 @@ typedef struct te_repair_object {
 /* Batched Slicer::repair of nobj lost slices (each with its own plan). */
 int te_repair_batch_device(te_clay *c, const uint8_t *d_helpers, const te_repair_object *objs,
                            size_t nobj, uint8_t *d_out, void *hip_stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Slice commitments: BlobEncoder::encode_with_proofs' step after encode
+ * (sdk/src/codec/encoder.rs:226-234) -- hash_leaf per slice, the merkle root and a proof per
+ * slice -- from lib/crypto/src/merkle/tree.rs.  Hashes are 32-byte SHA-256 digests.
+ * ------------------------------------------------------------------------------------------ */
+#define TE_HASH_SIZE 32
+#define TE_SLICE_TREE_HEIGHT 5          /* SLICE_TREE_HEIGHT      lib/core/src/erasure.rs:9  */
+#define TE_MAX_MERKLE_TREE_HEIGHT 32    /* MAX_MERKLE_TREE_HEIGHT tree.rs:6                  */
+#define TE_COMMIT_MAX_LEAVES 64         /* leaves per object in te_commit_batch_device       */
+
+/* hash_leaf (tree.rs:53-56): SHA-256("LEAF" || data).  Host. */
+int te_hash_leaf(const uint8_t *data, size_t len, uint8_t out[TE_HASH_SIZE]);
+/* hash_pair (tree.rs:58-62): SHA-256("LEFT" || left || "RIGHT" || right).  Host. */
+int te_hash_pair(const uint8_t left[TE_HASH_SIZE], const uint8_t right[TE_HASH_SIZE], uint8_t out[TE_HASH_SIZE]);
+/* empty_subtree_root / EMPTY_ROOTS[height] (tree.rs:15-48, 64-68), height < 32.  Host. */
+int te_empty_subtree_root(uint32_t height, uint8_t out[TE_HASH_SIZE]);
+/* root_from_leaf_hashes::<height> (tree.rs:344-350): count <= 2^height (else TREE_FULL). */
+int te_merkle_root_from_leaf_hashes(const uint8_t *hashes, size_t count, uint32_t height, uint8_t out[TE_HASH_SIZE]);
+/* create_proof_from_leaf_hashes::<height> (tree.rs:353-358, 397-455): `height` hashes. */
+int te_merkle_proof_from_leaf_hashes(const uint8_t *hashes, size_t count, size_t index, uint32_t height,
+                                     uint8_t *proof_out);
+/* verify_proof (tree.rs:462-481) over a pre-hashed leaf: 1 valid, 0 not valid. */
+int te_merkle_verify_leaf_hash(const uint8_t leaf_hash[TE_HASH_SIZE], const uint8_t root[TE_HASH_SIZE],
+                               const uint8_t *proof, size_t proof_len, uint64_t index, uint32_t height);
+/* Batched commitments on the device (DEVICE pointers, enqueued on hip_stream): object o's n
+ * slices at d_slices + o*obj_stride + i*slice_len (slice_len % 4 == 0, n <= 64) ->
+ * leaf hashes d_leaf_hashes[(o*n + i)*32], roots d_roots[o*32] (NULL: leaves only), proofs
+ * d_proofs[((o*n + i)*height + level)*32] (NULL: none). */
+int te_commit_batch_device(const uint8_t *d_slices, uint64_t obj_stride, uint64_t slice_len, uint32_t n,
+                           size_t nobj, uint32_t height, uint8_t *d_leaf_hashes, uint8_t *d_roots,
+                           uint8_t *d_proofs, void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -5,6 +5,7 @@ The compute lives in libtapeec.so (hand-written gfx950 HIP kernels behind the C 
 include/tape_ec.h).  This package is the Python host mirror of the reference's Rust API.
 """
 from ._lib import build, device_count, lib  # noqa: F401
+from .merkle import MerkleError, commit_batch, commit_slices, hash_leaf, hash_pair  # noqa: F401
 from .slicer import (  # noqa: F401
     ClayCoder, ClayParams, DecodeError, EncodeError, EncodingProfile, EncodingType, EngineError, HelperPlan,
     MappingStrategy, NoDeviceError, RepairError, RepairPlan, SliceMetadata, Slicer, StripeRepair,

@@ -24,6 +24,10 @@ TE_ERR_NOT_ENOUGH_HELPERS = 6
 TE_ERR_INVALID_SLICE = 7
 TE_ERR_CLAY = 8
 TE_ERR_MISSING_HELPER = 9
+TE_ERR_MERKLE_TREE_FULL = 10
+TE_ERR_MERKLE_INVALID_PROOF = 11
+TE_ERR_MERKLE_INVALID_INDEX = 12
+TE_ERR_MERKLE_PROOF_LENGTH = 13
 TE_ERR_INVALID_ARG = 20
 TE_ERR_NO_DEVICE = 21
 TE_ERR_HIP = 22
@@ -131,6 +135,13 @@ def _load() -> C.CDLL:
         "te_decode_batch_device": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_decode_object), u8p, sz,
                                        vp, vp]),
         "te_repair_batch_device": (i, [vp, vp, C.POINTER(te_repair_object), sz, vp, vp]),
+        "te_hash_leaf": (i, [u8p, sz, u8p]),
+        "te_hash_pair": (i, [u8p, u8p, u8p]),
+        "te_empty_subtree_root": (i, [u32, u8p]),
+        "te_merkle_root_from_leaf_hashes": (i, [u8p, sz, u32, u8p]),
+        "te_merkle_proof_from_leaf_hashes": (i, [u8p, sz, sz, u32, u8p]),
+        "te_merkle_verify_leaf_hash": (i, [u8p, u8p, u8p, sz, u64, u32]),
+        "te_commit_batch_device": (i, [vp, u64, u64, u32, sz, u32, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

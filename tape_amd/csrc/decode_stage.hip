@@ -74,9 +74,6 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
     // input slice byte offset of internal node i (= shard i, nu = 0) in lane i, rotated
     uint32_t sl_lane = lane + J.rot;
     sl_lane = (sl_lane >= a.n ? sl_lane - a.n : sl_lane) * (uint32_t)a.in_stride;
-    auto in_off = [&](uint32_t src) -> uint32_t {  // src = node | plane << 8
-        return __builtin_amdgcn_readlane(sl_lane, src & 0xffu) + ((src >> 8) & 0xffu) * sc;
-    };
     uint32_t kbase[NK];  // the known nodes' slices
 #pragma unroll
     for (int j = 0; j < NK; j++) kbase[j] = __builtin_amdgcn_readlane(sl_lane, H.knode[j]);
@@ -125,7 +122,6 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
     auto ldw = [&](uint32_t st) -> uint32_t { return progw[st * kDpWords]; };
     auto W = [](uint32_t v, int i) -> uint32_t { return __builtin_amdgcn_readlane(v, i); };
     const bool kd_l = lane >= kDpKd && lane < kDpKd + NK, ed_l = lane >= kDpEd && lane < kDpEd + NE;
-    const bool eo_l = lane >= kDpEo && lane < kDpEo + NE;
     // input offset of the partner load word x describes (known input partner, type-1 partner)
     auto vec_in = [&](uint32_t x) -> uint32_t {
         const uint32_t k = x >> 28;

@@ -15,7 +15,10 @@
 #include <algorithm>
 #include "../../include/tape_ec.h"
 #include "kernels.hpp"
+#include "sha256.hpp"
+#include <array>
 #include "clay_host.hpp"
+#include "sha256.hpp"
 
 using namespace tec;
 
@@ -252,6 +255,10 @@ const char *te_strerror(int s) {
         case TE_ERR_INVALID_SLICE: return "invalid slice index";
         case TE_ERR_CLAY: return "clay error";
         case TE_ERR_MISSING_HELPER: return "missing helper data";
+        case TE_ERR_MERKLE_TREE_FULL: return "merkle tree full";
+        case TE_ERR_MERKLE_INVALID_PROOF: return "invalid merkle proof";
+        case TE_ERR_MERKLE_INVALID_INDEX: return "invalid merkle leaf index";
+        case TE_ERR_MERKLE_PROOF_LENGTH: return "merkle proof length differs from the tree height";
         case TE_ERR_INVALID_ARG: return "invalid argument";
         case TE_ERR_NO_DEVICE: return "no gfx950 HIP device available (libtapeec has no CPU fallback)";
         case TE_ERR_HIP: return "HIP runtime error";
@@ -1310,6 +1317,126 @@ int te_clay_repair(te_clay *c, uint32_t lost, const uint32_t *helpers, const uin
     int r = te_slicer_repair(c, &p, by_slice.data(), lens.data(), meta, tmp.data(), tmp.size());
     if (r) return r;
     memcpy(out, tmp.data(), chunk_size);
+    return TE_OK;
+}
+
+
+// ---- slice commitments (lib/crypto/src/merkle/tree.rs) ----
+int te_hash_leaf(const uint8_t *data, size_t len, uint8_t out[TE_HASH_SIZE]) {
+    if ((!data && len) || !out) return TE_ERR_INVALID_ARG;
+    sha::hash_leaf(data, len, out);
+    return TE_OK;
+}
+
+int te_hash_pair(const uint8_t left[TE_HASH_SIZE], const uint8_t right[TE_HASH_SIZE], uint8_t out[TE_HASH_SIZE]) {
+    if (!left || !right || !out) return TE_ERR_INVALID_ARG;
+    sha::hash_pair(left, right, out);
+    return TE_OK;
+}
+
+int te_empty_subtree_root(uint32_t height, uint8_t out[TE_HASH_SIZE]) {
+    if (height >= TE_MAX_MERKLE_TREE_HEIGHT || !out) return TE_ERR_INVALID_ARG;
+    sha::empty_root(height, out);
+    return TE_OK;
+}
+
+// MerkleTree::<N>::new() + add_leaf_hash per leaf (tree.rs:86-153, 344-350)
+int te_merkle_root_from_leaf_hashes(const uint8_t *hashes, size_t count, uint32_t height, uint8_t out[TE_HASH_SIZE]) {
+    if (height == 0 || height > TE_MAX_MERKLE_TREE_HEIGHT || (!hashes && count) || !out) return TE_ERR_INVALID_ARG;
+    if (height < 64 && (uint64_t)count > (1ull << height)) return TE_ERR_MERKLE_TREE_FULL;
+    std::vector<std::array<uint8_t, 32>> empty(height), filled(height);
+    for (uint32_t l = 0; l < height; l++) {
+        sha::empty_root(l, empty[l].data());
+        filled[l] = empty[l];
+    }
+    std::array<uint8_t, 32> root = empty[height - 1];
+    for (size_t index = 0; index < count; index++) {
+        std::array<uint8_t, 32> cur, t;
+        memcpy(cur.data(), hashes + index * 32, 32);
+        uint64_t idx = index;
+        for (uint32_t l = 0; l < height; l++) {
+            if ((idx & 1) == 0) {
+                filled[l] = cur;
+                sha::hash_pair(cur.data(), empty[l].data(), t.data());
+            } else {
+                sha::hash_pair(filled[l].data(), cur.data(), t.data());
+            }
+            cur = t;
+            idx >>= 1;
+        }
+        root = cur;
+    }
+    memcpy(out, root.data(), 32);
+    return TE_OK;
+}
+
+// create_merkle_proof_hashes (tree.rs:397-455)
+int te_merkle_proof_from_leaf_hashes(const uint8_t *hashes, size_t count, size_t index, uint32_t height,
+                                     uint8_t *proof_out) {
+    if (!proof_out) return TE_ERR_INVALID_ARG;
+    if (!hashes || count == 0 || index >= count || height > TE_MAX_MERKLE_TREE_HEIGHT ||
+        (height < 64 && (uint64_t)count > (1ull << height)))
+        return TE_ERR_MERKLE_INVALID_PROOF;
+    std::vector<std::array<uint8_t, 32>> cur(count);
+    for (size_t i = 0; i < count; i++) memcpy(cur[i].data(), hashes + i * 32, 32);
+    std::array<uint8_t, 32> empty;
+    sha::empty_root(0, empty.data());
+    size_t ci = index;
+    for (uint32_t l = 0; l < height; l++) {
+        if (cur.size() % 2) cur.push_back(empty);
+        memcpy(proof_out + (size_t)l * 32, cur[ci ^ 1].data(), 32);
+        std::vector<std::array<uint8_t, 32>> next(cur.size() / 2);
+        for (size_t j = 0; j < next.size(); j++) sha::hash_pair(cur[2 * j].data(), cur[2 * j + 1].data(), next[j].data());
+        cur.swap(next);
+        std::array<uint8_t, 32> e2;
+        sha::hash_pair(empty.data(), empty.data(), e2.data());
+        empty = e2;
+        ci >>= 1;
+    }
+    return TE_OK;
+}
+
+// verify_proof (tree.rs:462-481), leaf already hashed
+int te_merkle_verify_leaf_hash(const uint8_t leaf_hash[TE_HASH_SIZE], const uint8_t root[TE_HASH_SIZE],
+                               const uint8_t *proof, size_t proof_len, uint64_t index, uint32_t height) {
+    if (!leaf_hash || !root || (!proof && proof_len)) return TE_ERR_INVALID_ARG;
+    if (proof_len != height) return 0;
+    uint8_t node[32], t[32];
+    memcpy(node, leaf_hash, 32);
+    uint64_t idx = index;
+    for (size_t i = 0; i < proof_len; i++) {
+        if ((idx & 1) == 0) sha::hash_pair(node, proof + i * 32, t);
+        else sha::hash_pair(proof + i * 32, node, t);
+        memcpy(node, t, 32);
+        idx >>= 1;
+    }
+    return memcmp(node, root, 32) == 0 ? 1 : 0;
+}
+
+int te_commit_batch_device(const uint8_t *d_slices, uint64_t obj_stride, uint64_t slice_len, uint32_t n,
+                           size_t nobj, uint32_t height, uint8_t *d_leaf_hashes, uint8_t *d_roots,
+                           uint8_t *d_proofs, void *stream) {
+    if (nobj == 0) return TE_OK;
+    if (!d_slices || !d_leaf_hashes || n == 0 || n > TE_COMMIT_MAX_LEAVES || slice_len % 4 ||
+        nobj > 0xffffffffull / n || ((d_roots || d_proofs) && (height == 0 || height > TE_MAX_MERKLE_TREE_HEIGHT)) ||
+        (d_proofs && !d_roots))
+        return TE_ERR_INVALID_ARG;
+    if ((d_roots || d_proofs) && height < 64 && (uint64_t)n > (1ull << height)) return TE_ERR_MERKLE_TREE_FULL;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    CommitArgs a{};
+    a.slices = d_slices;
+    a.obj_stride = obj_stride;
+    a.slice_len = slice_len;
+    a.n = n;
+    a.nobj = (uint32_t)nobj;
+    a.height = height;
+    a.leaf = d_leaf_hashes;
+    a.root = d_roots;
+    a.proof = d_proofs;
+    hipStream_t s = (hipStream_t)stream;
+    KTimer kt(s);
+    TE_HIP(launch_commit(a, s));
+    kt.stop();
     return TE_OK;
 }
 

@@ -187,6 +187,18 @@ uint32_t decode_stage_rows(uint32_t nslots, uint32_t max_out);  // LDS rows of a
 bool decode_stage_fits(uint32_t nslots, uint32_t max_out);
 bool decode_stage_k(int k);  // a staged-decode kernel is compiled for this k (n = 20)
 
+// ---- slice commitments (commit.hip) ----
+constexpr int kCommitMaxLeaves = 64;
+struct CommitArgs {
+    const uint8_t *slices;     // object o's slice i at slices + o * obj_stride + i * slice_len
+    uint64_t obj_stride, slice_len;  // slice_len % 4 == 0
+    uint32_t n, nobj, height;
+    uint8_t *leaf;             // nobj * n * 32
+    uint8_t *root;             // nobj * 32, or null (no tree)
+    uint8_t *proof;            // nobj * n * height * 32, or null
+};
+hipError_t launch_commit(const CommitArgs &a, hipStream_t s);
+
 hipError_t launch_encode_rows(int k, bool masked, const EncArgs &a, hipStream_t s);
 hipError_t launch_meta(const MetaJob *jobs, uint32_t njobs, uint32_t n, hipStream_t s);
 hipError_t launch_gpe(const GpeArgs &a, uint32_t max_erased, hipStream_t s);

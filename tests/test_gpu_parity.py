@@ -299,3 +299,57 @@ def test_batch_encode_host_pipeline(oracle, o716, pinned):
     batch.encode_batch(s, h_in.to("cuda:0"), objs, d_out)
     torch.cuda.synchronize()
     assert np.array_equal(d_out.cpu().numpy(), out)
+
+
+# ---------------------------------------------------------------- commitments (§8f-1) -------
+@pytest.mark.parametrize("slen", [4, 8, 52, 56, 60, 64, 116, 120, 124, 1000, 14_448, 286_048, 715_048])
+def test_commit_batch_matches_oracle(slen):
+    import torch
+    from oracle import merkle_oracle as O
+    from tape_amd import merkle
+    n, nobj, H = 20, 3, 5
+    host = torch.from_numpy(np.frombuffer(np.random.default_rng(slen).bytes(nobj * n * slen), dtype=np.uint8).copy())
+    dev = host.cuda()
+    leaf = torch.empty(nobj * n * 32, dtype=torch.uint8, device="cuda")
+    root = torch.empty(nobj * 32, dtype=torch.uint8, device="cuda")
+    proof = torch.empty(nobj * n * H * 32, dtype=torch.uint8, device="cuda")
+    merkle.commit_batch(dev, n * slen, slen, n, nobj, leaf, root, proof, H)
+    torch.cuda.synchronize()
+    lb, rb, pb = (t.cpu().numpy().tobytes() for t in (leaf, root, proof))
+    raw = host.numpy().tobytes()
+    for o in range(nobj):
+        sl = [raw[(o * n + i) * slen:(o * n + i + 1) * slen] for i in range(n)]
+        leaves, r, proofs = O.commit_slices(sl, H)
+        assert lb[o * n * 32:(o + 1) * n * 32] == b"".join(leaves), (slen, o)
+        assert rb[o * 32:(o + 1) * 32] == r, (slen, o)
+        got = [[pb[((o * n + i) * H + l) * 32:((o * n + i) * H + l + 1) * 32] for l in range(H)] for i in range(n)]
+        assert got == proofs, (slen, o)
+
+
+def test_encode_with_proofs_4mib(oracle):  # BlobEncoder::encode_with_proofs, encoder.rs:220-234
+    from oracle import merkle_oracle as O
+    from tape_amd import merkle
+    data = oracle.splitmix64_bytes(99, 4 * MiB).tobytes()
+    sl = T.Slicer.clay_default().encode(data)
+    leaves, root, proofs = merkle.commit_slices(sl)
+    exp = O.commit_slices(sl)
+    assert (leaves, root, proofs) == exp
+    for i in range(N):
+        assert merkle.verify_proof(sl[i], root, proofs[i], i)
+
+
+def test_commit_leaves_only_and_partial_wave():
+    import torch
+    from oracle import merkle_oracle as O
+    from tape_amd import merkle
+    n, nobj, slen = 7, 5, 1_000  # 35 streams: a partial wave
+    host = torch.from_numpy(np.frombuffer(np.random.default_rng(1).bytes(nobj * n * slen + 64), dtype=np.uint8).copy())
+    dev = host.cuda()
+    leaf = torch.empty(nobj * n * 32, dtype=torch.uint8, device="cuda")
+    merkle.commit_batch(dev, n * slen + 8, slen, n, nobj, leaf)  # obj_stride != n * slice_len
+    torch.cuda.synchronize()
+    raw, lb = host.numpy().tobytes(), leaf.cpu().numpy().tobytes()
+    for o in range(nobj):
+        for i in range(n):
+            off = o * (n * slen + 8) + i * slen
+            assert lb[(o * n + i) * 32:(o * n + i + 1) * 32] == O.hash_leaf(raw[off:off + slen])
