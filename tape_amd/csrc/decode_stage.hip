@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
         const uint32_t r_beg = (wv * no) / G, r_end = ((wv + 1) * no) / G;
         for (uint32_t r = r_beg; r < r_end && !(TEC_DEC_ABLATE & 4); r++) {
             const uint8_t *row = lds8 + (sbase + r) * RS;
-            const uint32_t it = (__builtin_amdgcn_readlane(w_cur, kDpOut + (r >> 1)) >> (16u * (r & 1u))) & 0xffffu;
+            const uint32_t it = ((uint32_t)__builtin_amdgcn_readlane(w_cur, kDpOut + (r >> 1)) >> (16u * (r & 1u))) & 0xffffu;
             const uint32_t off = (it & 0xffu) * (uint32_t)a.out_stride + (it >> 8) * sc + seg0;
             flush16(row, lane, off);
             if (RS > 1024u) flush16(row, lane + 64u, off);
