@@ -11,7 +11,7 @@ import json
 import os
 import sys
 
-OURS = ("enc_stage", "dec_stage", "rep_stage", "gpe_kernel", "repair_kernel", "meta_kernel")
+OURS = ("enc_stage", "dec_stage", "rep_stage", "leaf_kernel", "tree_kernel", "gpe_kernel", "repair_kernel", "meta_kernel")
 
 
 def kernel_stats(d):
