@@ -176,7 +176,16 @@ template <int G>
 __constant__ Col1Off<G> Col1Holder<G>::tab = make_col1_off<G>();
 
 #ifndef TEC_STAGE_ST_AUX
-#define TEC_STAGE_ST_AUX 0  // cache policy of the slice stores (gfx950: 2 = nt, 16 = sc1)
+#define TEC_STAGE_ST_AUX 2  // cache policy of the slice stores (gfx950: 2 = nt, 16 = sc1): nt measured 2 % faster
+#endif
+#ifndef TEC_STAGE_PRIO
+#define TEC_STAGE_PRIO 1  // wave priority during a step's compute (s_setprio), 0 = off
+#endif
+#ifndef TEC_STAGE_OWN_AUX
+#define TEC_STAGE_OWN_AUX 0  // cache policy of the level-1 own-row loads
+#endif
+#ifndef TEC_STAGE_PART_AUX
+#define TEC_STAGE_PART_AUX 0  // cache policy of the level-1 partner-row loads
 #endif
 #ifndef TEC_STAGE_PF
 #define TEC_STAGE_PF 1  // planes of load lookahead (1 or 2)
@@ -332,13 +341,13 @@ __global__ void __launch_bounds__(G * 64, TEC_STAGE_WAVES_PER_EU) enc_stage_kern
     auto load_own_to = [&](uint32_t(&o)[K], uint32_t z0, uint32_t s) {
         const uint32_t so = src_al + (z0 * kQ + s) * sc;
 #pragma unroll
-        for (int x = 0; x < K; x++) o[x] = gload(rs_src, vo_own[x], so);
+        for (int x = 0; x < K; x++) o[x] = gload<TEC_STAGE_OWN_AUX>(rs_src, vo_own[x], so);
     };
     auto load_part_to = [&](uint32_t(&part)[kQ], uint32_t z0, uint32_t s) {
         if (z0 < (uint32_t)K) {
             const uint32_t so = src_al + z0 * cs + s * sc;
 #pragma unroll
-            for (int x = 0; x < kQ; x++) part[x] = gload(rs_src, vo_part[x], so);
+            for (int x = 0; x < kQ; x++) part[x] = gload<TEC_STAGE_PART_AUX>(rs_src, vo_part[x], so);
         } else {
             // level-1 outputs of other waves: written before the level-1 -> level-2 drain
             // (vmcnt(0) + barrier); nt loads skip this CU's L1
@@ -494,6 +503,7 @@ __global__ void __launch_bounds__(G * 64, TEC_STAGE_WAVES_PER_EU) enc_stage_kern
             }
             if (z0 < (uint32_t)K) {
                 // ---- level 1: data partners are inputs; column-0 parity by type-1 recovery ----
+                if constexpr (TEC_STAGE_PRIO) __builtin_amdgcn_s_setprio(TEC_STAGE_PRIO);
                 uint32_t u[K];
 #pragma unroll
                 for (int x = 0; x < K; x++) {
@@ -505,6 +515,7 @@ __global__ void __launch_bounds__(G * 64, TEC_STAGE_WAVES_PER_EU) enc_stage_kern
 #pragma unroll
                 for (int r = K; r < kQ; r++) stage(r, acc[r - K] ^ mulc(kPft.t_p[1], cpart[r]));
                 col1(acc + NP0, s);
+                if constexpr (TEC_STAGE_PRIO) __builtin_amdgcn_s_setprio(0);
                 step_barrier();  // B2: the step's rows are staged
                 flush(FT.w[0][s][wv], z0);
                 if (boundary) {
@@ -515,6 +526,7 @@ __global__ void __launch_bounds__(G * 64, TEC_STAGE_WAVES_PER_EU) enc_stage_kern
                 }
             } else if constexpr (NP0 > 0) {
                 // ---- level 2: data partners are the level-1 column-0 parity C(z0, (x, s)) ----
+                if constexpr (TEC_STAGE_PRIO) __builtin_amdgcn_s_setprio(TEC_STAGE_PRIO);
                 uint32_t u[K];
 #pragma unroll
                 for (int x = 0; x < K; x++) {
@@ -544,6 +556,7 @@ __global__ void __launch_bounds__(G * 64, TEC_STAGE_WAVES_PER_EU) enc_stage_kern
                                                               (int)((pidx(z0, r) * kQ + s) * RS), 0);
                 }
                 col1(acc + NP0, s);
+                if constexpr (TEC_STAGE_PRIO) __builtin_amdgcn_s_setprio(0);
                 step_barrier();
                 flush(FT.w[1 + i0][s][wv], z0);
             }
