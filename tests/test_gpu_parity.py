@@ -42,7 +42,8 @@ def test_clay_encode_matches_oracle(oracle, params, ln):
     assert c.encode(data) == o.encode(data)
 
 
-@pytest.mark.parametrize("params", [(20, 7, 16), (20, 10, 19), (20, 5, 14), (12, 8, 11), (20, 7, 19)])
+@pytest.mark.parametrize("params", [(20, 7, 16), (20, 8, 17), (20, 9, 18), (20, 10, 19), (20, 5, 14), (12, 8, 11),
+                                    (20, 7, 19)])
 def test_clay_decode_any_k(oracle, params):
     c = T.ClayCoder(*params)
     n, k, _ = params
@@ -353,3 +354,20 @@ def test_commit_leaves_only_and_partial_wave():
         for i in range(n):
             off = o * (n * slen + 8) + i * slen
             assert lb[(o * n + i) * 32:(o * n + i + 1) * 32] == O.hash_leaf(raw[off:off + slen])
+
+
+@pytest.mark.parametrize("params", [(20, 7, 16), (20, 8, 17), (20, 9, 18), (20, 10, 19)])
+def test_clay_decode_many_patterns_vs_oracle(oracle, params):
+    # staged decode (one plane program per erasure pattern, kernels for k = 7..10) against the
+    # oracle's own decode on 60 random survivor sets of exactly k .. n-1 chunks
+    c = T.ClayCoder(*params)
+    o = oracle.OracleClay(*params)
+    n, k, _ = params
+    data = oracle.splitmix64_bytes(k * 1000 + 7, 30_000).tobytes()
+    ch = c.encode(data)
+    assert ch == o.encode(data)
+    rnd = random.Random(k)
+    for _ in range(60):
+        keep = sorted(rnd.sample(range(n), rnd.choice([k, k, k + 1, rnd.randint(k, n - 1)])))
+        got = c.decode([(i, ch[i]) for i in keep])
+        assert got[:len(data)] == data, keep
