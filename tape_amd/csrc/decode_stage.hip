@@ -227,7 +227,7 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
 #pragma unroll
             for (int j = 0; j < NK; j++)
                 if (TEC_DEC_ABLATE & 2) acc[e] ^= sel[j].s0 + e; else
-                acc[e] ^= perm_mul(sel[j], D[e][j].t[0], D[e][j].t[1], D[e][j].t[2], D[e][j].t[3]);
+                acc[e] = perm_mul_acc(acc[e], sel[j], D[e][j].t[0], D[e][j].t[1], D[e][j].t[2], D[e][j].t[3]);
         }
         // ---- writes: lane A of a word is its general destination (known: kout; erased: the
         // park location; eo: ed0), B and C the staging-only ed1 / epd ----

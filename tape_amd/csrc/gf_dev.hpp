@@ -64,6 +64,17 @@ __device__ __forceinline__ uint32_t perm_mul(const Sel &s, uint32_t t0, uint32_t
     return a ^ b ^ c ^ d;
 }
 
+// acc ^ c * x in six VALU: four v_perm and two v_bitop3 XOR3 (the backend does not form XOR3
+// from the plain expression, which costs four v_xor_b32)
+__device__ __forceinline__ uint32_t perm_mul_acc(uint32_t acc, const Sel &s, uint32_t t0, uint32_t t1, uint32_t t2,
+                                                 uint32_t t3) {
+    const uint32_t a = __builtin_amdgcn_perm(t0, t0, s.s0);
+    const uint32_t b = __builtin_amdgcn_perm(t1, t1, s.s1);
+    const uint32_t c = __builtin_amdgcn_perm(t2, t2, s.s2);
+    const uint32_t d = __builtin_amdgcn_perm(t3, t3, s.s3);
+    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(acc, a, b, 0x96), c, d, 0x96);
+}
+
 __device__ __forceinline__ uint32_t perm_mul(const Sel &s, const PermTab &t) {
     return perm_mul(s, t.t[0], t.t[1], t.t[2], t.t[3]);
 }
