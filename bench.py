@@ -7,8 +7,9 @@ profile Clay(20,7,16), rotated 1 MB stripes; one "step" = one te_encode_batch_de
 the whole batch (all 20 slices incl. metadata written to HBM).  Multi-GPU (torchrun): objects
 are partitioned across ranks (per-GPU batches, weak scaling), no data-path collective.
 
-Also: --mode repair (config 3), --mode decode (config 4, slices 0..12 erased) and --mode commit
-(hash_leaf of the 20 slices + merkle root + proofs of every encoded object).
+Also: --mode repair (config 3), --mode decode (config 4, slices 0..12 erased), --mode commit
+(hash_leaf of the 20 slices + merkle root + proofs of every encoded object) and
+--mode recover (decode from 7 slices + re-encode, the node's recover path).
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
@@ -31,6 +32,8 @@ ALG_BYTES = {  # algorithmic HBM bytes per 4 MiB object
     "repair": 16 * 71_500 + 715_048,
     "decode": 7 * 715_048 + 4 * MiB,
     "commit": N * 715_048 + N * 32 + 32 + N * 5 * 32,  # slices read; leaf hashes, root, proofs written
+    # decode (7 slices in, object out) + encode (object in, 20 slices out) + the lost slice copied
+    "recover": (7 * 715_048 + 4 * MiB) + (4 * MiB + N * 715_048) + 2 * 715_048,
 }
 
 
@@ -99,7 +102,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--objects", type=int, default=1024, help="objects per GPU per step")
     ap.add_argument("--object-bytes", type=int, default=4 * MiB)
-    ap.add_argument("--mode", choices=["encode", "repair", "decode", "commit"], default="encode")
+    ap.add_argument("--mode", choices=["encode", "repair", "decode", "commit", "recover"], default="encode")
     ap.add_argument("--cpu-sample", type=int, default=96, help="objects in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity cores)")
     ap.add_argument("--copy-objects", type=int, default=256,
@@ -174,6 +177,15 @@ def main():
         def step():
             batch.repair_batch(slicer.coder, d_help, rep_objs, d_rep, stream)
 
+    elif args.mode == "recover":  # lost = i mod 20 from the 7 slices after it (recover.rs:411-442)
+        metas = b"".join(d_out[i * per + g.slice_len - 48:i * per + g.slice_len].cpu().numpy().tobytes()
+                         for i in range(nobj))
+        d_rec = torch.empty(nobj * g.slice_len, dtype=torch.uint8, device=dev)
+        rec_objs = [(i * per, g.slice_len, sum(1 << ((i + j) % N) for j in range(1, 8)), i % N, i * g.slice_len)
+                    for i in range(nobj)]
+
+        def step():
+            batch.recover_batch(slicer, d_out, rec_objs, metas, d_rec, stream)
     elif args.mode == "commit":
         from tape_amd import merkle
         d_leaf = torch.empty(nobj * N * 32, dtype=torch.uint8, device=dev)
@@ -207,7 +219,8 @@ def main():
 
     total_objs = nobj * world * args.steps
     gib_s = total_objs * L / elapsed / 2**30
-    avg_launch_s = kms / max(1, kcalls) / 1e3
+    # device time of one step's kernels (recover = a decode and an encode enqueue per step)
+    avg_launch_s = kms / max(1, args.steps) / 1e3
     achieved = (unit_bytes or 0) * nobj / avg_launch_s / 1e9 if unit_bytes else None
 
     verified = None  # the timed outputs, checked on the device against what they must equal
@@ -217,6 +230,11 @@ def main():
         sl = g.slice_len
         ref = torch.stack([d_out[i * per + (i % N) * sl:i * per + (i % N + 1) * sl] for i in range(nobj)])
         verified = bool(torch.equal(d_rep.view(nobj, sl), ref))
+        del ref
+    elif args.mode == "recover":
+        sl = g.slice_len
+        ref = torch.stack([d_out[i * per + (i % N) * sl:i * per + (i % N + 1) * sl] for i in range(nobj)])
+        verified = bool(torch.equal(d_rec.view(nobj, sl), ref))
         del ref
     elif args.mode == "commit":  # first and last object against hashlib (SHA-256 of "LEAF" || slice)
         import hashlib
@@ -263,7 +281,8 @@ def main():
             "data": "synthetic (SplitMix64 per object, seed 0x7A9E5EED ^ id), device-resident",
             "config": {"workload": {"encode": "Slicer::encode", "repair": "Slicer::repair (lost = i mod 20)",
                                     "decode": "Slicer::decode (slices 0..12 erased)",
-                                    "commit": "encode_with_proofs commitment (SHA-256 leaf per slice, height-5 root, 20 proofs)"}[args.mode]
+                                    "commit": "encode_with_proofs commitment (SHA-256 leaf per slice, height-5 root, 20 proofs)",
+                                    "recover": "node recover (decode from 7 slices + re-encode, lost = i mod 20)"}[args.mode]
                        + f" of {nobj} x {L} B objects per GPU, Clay(20,7,16) rotated, 1 MB stripes",
                        "objects_per_gpu": nobj, "object_bytes": L, "profile": "clay(20,7,16)",
                        "parallelism": f"objects partitioned over {world} GPU(s)"},

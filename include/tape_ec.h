@@ -233,6 +233,20 @@ typedef struct te_repair_object {
 int te_repair_batch_device(te_clay *c, const uint8_t *d_helpers, const te_repair_object *objs,
                            size_t nobj, uint8_t *d_out, void *hip_stream);
 
+typedef struct te_recover_object {
+    uint64_t slices_off;  /* peer slice i at d_slices + slices_off + i*slice_len (if in avail_mask) */
+    uint64_t slice_len;
+    uint32_t avail_mask;  /* bit i set = slice i present (>= k of them) */
+    uint32_t lost;        /* slice index to rebuild */
+    uint64_t out_off;     /* the rebuilt slice (slice_len bytes) at d_out + out_off */
+} te_recover_object;
+/* Batched node recover, network/node/src/features/spool/recover.rs:411-442 `reconstruct`
+ * (SURVEY §8f-2): Slicer::decode from the peer slices, Slicer::encode of the object with the
+ * peers' chunk_index, keep slice `lost`.  h_meta: one 48-byte suffix per object (host). */
+int te_recover_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices,
+                            const te_recover_object *objs, const uint8_t *h_meta, size_t nobj,
+                            uint8_t *d_out, void *hip_stream);
+
 /* ------------------------------------------------------------------------------------------
  * Slice commitments: BlobEncoder::encode_with_proofs' step after encode
  * (sdk/src/codec/encoder.rs:226-234) -- hash_leaf per slice, the merkle root and a proof per

@@ -6,7 +6,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/round
 mkdir -p $OUT
-for m in repair decode commit; do
+for m in repair decode commit recover; do
   timeout -k 10 400 python bench.py --mode $m > $OUT/bench_$m.json 2> $OUT/bench_$m.err || exit $?
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$m -o run -- \
       python3 bench.py --mode $m --steps 5 --warmup 2 > $OUT/trace_$m.log 2>&1 || exit $?

@@ -68,6 +68,11 @@ class te_decode_object(C.Structure):
                 ("pad_", C.c_uint32), ("out_off", C.c_uint64)]
 
 
+class te_recover_object(C.Structure):
+    _fields_ = [("slices_off", C.c_uint64), ("slice_len", C.c_uint64), ("avail_mask", C.c_uint32),
+                ("lost", C.c_uint32), ("out_off", C.c_uint64)]
+
+
 class te_repair_object(C.Structure):
     _fields_ = [("plan", C.c_void_p), ("helper_off", C.c_uint64 * 20), ("out_off", C.c_uint64),
                 ("metadata", C.c_uint8 * 48)]
@@ -135,6 +140,8 @@ def _load() -> C.CDLL:
         "te_decode_batch_device": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_decode_object), u8p, sz,
                                        vp, vp]),
         "te_repair_batch_device": (i, [vp, vp, C.POINTER(te_repair_object), sz, vp, vp]),
+        "te_recover_batch_device": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_recover_object), u8p, sz,
+                                        vp, vp]),
         "te_hash_leaf": (i, [u8p, sz, u8p]),
         "te_hash_pair": (i, [u8p, u8p, u8p]),
         "te_empty_subtree_root": (i, [u32, u8p]),

@@ -82,6 +82,38 @@ def decode_batch(slicer: Slicer, slices, objs, metas: bytes, out, stream=None) -
     _check(r, "decode")
 
 
+def recover_batch(slicer: Slicer, slices, objs: list[tuple[int, int, int, int, int]], metas: bytes, out,
+                  stream=None) -> None:
+    """Node recover (recover.rs:411-442 `reconstruct`) on the device: objs are (slices_off,
+    slice_len, avail_mask, lost, out_off); metas nobj*48 metadata bytes (host)."""
+    arr = (_lib.te_recover_object * len(objs))(*[_lib.te_recover_object(*o) for o in objs])
+    cfg = slicer._cfg()
+    mb = (C.c_uint8 * max(1, len(metas))).from_buffer_copy(metas if metas else b"\0")
+    r = lib.te_recover_batch_device(slicer.coder.handle, C.byref(cfg), C.c_void_p(slices.data_ptr()), arr, mb,
+                                    len(arr), C.c_void_p(out.data_ptr()), _stream_ptr(stream))
+    _check(r, "decode")
+
+
+def reconstruct(slicer: Slicer, lost: int, peer_slices: list[tuple[int, bytes]]) -> bytes:
+    """recover.rs:411-442 `reconstruct`: decode the peers' slices, re-encode, return slice `lost`
+    (one object, host bytes in and out, through recover_batch)."""
+    import torch
+    if not peer_slices:
+        raise ValueError("no peer slices provided")
+    slen = len(peer_slices[0][1])
+    n = slicer.coder.n()
+    host = bytearray(n * slen)
+    mask = 0
+    for i, d in peer_slices:
+        host[i * slen:(i + 1) * slen] = d
+        mask |= 1 << i
+    dev = torch.frombuffer(host, dtype=torch.uint8).cuda()
+    out = torch.empty(slen, dtype=torch.uint8, device="cuda")
+    recover_batch(slicer, dev, [(0, slen, mask, lost, 0)], bytes(peer_slices[0][1][-48:]), out)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().tobytes()
+
+
 def repair_descs(objs: list[tuple[RepairPlan, dict[int, int], int, bytes]]):
     """Prepared te_repair_object array for repair_batch (build once, reuse; the plans must stay
     alive while it is used)."""

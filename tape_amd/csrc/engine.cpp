@@ -222,6 +222,7 @@ struct te_clay {
     hipStream_t stream = nullptr;  // for the synchronous host-buffer entry points
     Arena enc, dec, rep;
     DevBuf io_in, io_out;          // staging for host-buffer entry points
+    DevBuf rec_blob, rec_slices;   // te_recover_batch_device: decoded objects, re-encoded slices
     // te_encode_batch_host pipeline: kPipe slots, each with its own stream, descriptor arena
     // and device window buffers, so window w+1's H2D overlaps window w's kernel and D2H.
     static constexpr int kPipe = 3;
@@ -1044,6 +1045,49 @@ int te_repair_batch_device(te_clay *c, const uint8_t *d_helpers, const te_repair
     }
     std::lock_guard<std::mutex> lk(c->mu);
     return repair_enqueue(c, d_helpers, items.data(), items.size(), d_out, (hipStream_t)stream);
+}
+
+// Node recover (network/node/src/features/spool/recover.rs:411-442 `reconstruct`): decode the
+// object from >= k peer slices, re-encode it, keep the lost slice.  Decode and encode run back to
+// back on the stream through device workspaces; only the lost slice leaves them.
+int te_recover_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices,
+                            const te_recover_object *objs, const uint8_t *h_meta, size_t nobj, uint8_t *d_out,
+                            void *stream) {
+    if (!c || !cfg || (!objs && nobj) || (!h_meta && nobj)) return TE_ERR_INVALID_ARG;
+    if (nobj == 0) return TE_OK;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    const uint32_t n = (uint32_t)c->h.n;
+    std::vector<DecItem> items(nobj);
+    std::vector<te_object> enc(nobj);
+    uint64_t blob_total = 0, slice_total = 0;
+    for (size_t i = 0; i < nobj; i++) {
+        if (objs[i].lost >= n) return TE_ERR_INVALID_SLICE;
+        int r = decode_validate(c, h_meta + i * TE_META_SIZE, objs[i].slice_len, objs[i].avail_mask, items[i]);
+        if (r) return r;
+        te_slice_metadata m;
+        te_slice_metadata_from_slice(h_meta + i * TE_META_SIZE, TE_META_SIZE, &m);
+        te_geometry g;
+        te_slicer_geometry(c, items[i].blob_len, &g);
+        if (g.slice_len != objs[i].slice_len) return TE_ERR_INVALID_LAYOUT;
+        items[i].in_base = objs[i].slices_off;
+        items[i].out_off = blob_total;
+        enc[i] = te_object{blob_total, items[i].blob_len, slice_total, m.chunk_index};
+        blob_total += (items[i].blob_len + 15) & ~15ull;
+        slice_total += (uint64_t)n * g.slice_len;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t s = (hipStream_t)stream;
+    TE_HIP(c->rec_blob.ensure(blob_total + 16));
+    TE_HIP(c->rec_slices.ensure(slice_total + 16));
+    int r = decode_enqueue(c, cfg, d_slices, items.data(), nobj, c->rec_blob.as<uint8_t>(), s, false);
+    if (r) return r;
+    r = encode_enqueue(c, cfg, c->rec_blob.as<uint8_t>(), enc.data(), nobj, c->rec_slices.as<uint8_t>(), s, false);
+    if (r) return r;
+    for (size_t i = 0; i < nobj; i++)
+        TE_HIP(hipMemcpyAsync(d_out + objs[i].out_off,
+                              c->rec_slices.as<uint8_t>() + enc[i].out_off + (uint64_t)objs[i].lost * objs[i].slice_len,
+                              objs[i].slice_len, hipMemcpyDeviceToDevice, s));
+    return TE_OK;
 }
 
 int te_slicer_encode(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *data, size_t len, uint8_t *slices,

@@ -371,3 +371,44 @@ def test_clay_decode_many_patterns_vs_oracle(oracle, params):
         keep = sorted(rnd.sample(range(n), rnd.choice([k, k, k + 1, rnd.randint(k, n - 1)])))
         got = c.decode([(i, ch[i]) for i in keep])
         assert got[:len(data)] == data, keep
+
+
+# ---------------------------------------------------------------- node recover (§8f-2) ------
+@pytest.mark.parametrize("ln", [1, 999, 100_003, 1_000_001, 4 * MiB])
+def test_reconstruct_matches_original_slice(oracle, ln):  # recover.rs:411-442
+    from tape_amd import batch
+    data = oracle.splitmix64_bytes(ln ^ 0xC0FFEE, ln).tobytes()
+    s = T.Slicer.clay_default()
+    s.set_chunk_index(3)
+    sl = s.encode(data)
+    rnd = random.Random(ln)
+    for lost in (0, 6, 7, 19, rnd.randrange(N)):
+        avail = sorted(rnd.sample([i for i in range(N) if i != lost], rnd.choice([7, 10, 19])))
+        got = batch.reconstruct(T.Slicer.clay_default(), lost, [(i, sl[i]) for i in avail])
+        assert got == sl[lost], (lost, avail)
+
+
+def test_recover_batch_device(oracle):
+    from tape_amd import batch
+    nobj, L = 6, 300_000
+    s = T.Slicer.clay_default()
+    g = s.geometry(L)
+    per = N * g.slice_len
+    host = bytearray()
+    metas = b""
+    objs, exp = [], []
+    rnd = random.Random(11)
+    for o in range(nobj):
+        sl = s.encode(oracle.splitmix64_bytes(o + 1, L).tobytes())
+        host += b"".join(sl)
+        lost = rnd.randrange(N)
+        avail = rnd.sample([i for i in range(N) if i != lost], 7 + o)
+        mask = sum(1 << i for i in avail)
+        objs.append((o * per, g.slice_len, mask, lost, o * g.slice_len))
+        exp.append(sl[lost])
+        metas += sl[0][-48:]
+    dev = torch.frombuffer(host, dtype=torch.uint8).cuda()
+    out = torch.empty(nobj * g.slice_len, dtype=torch.uint8, device="cuda")
+    batch.recover_batch(s, dev, objs, metas, out)
+    torch.cuda.synchronize()
+    assert out.cpu().numpy().tobytes() == b"".join(exp)

@@ -145,3 +145,18 @@ def test_kernel_timing_api_without_device():
     assert lib.te_kernel_time_ms(C.byref(ms), C.byref(n)) == 0
     assert ms.value == 0.0 and n.value == 0
     assert lib.te_kernel_timing(0) == 0
+
+
+def test_recover_needs_device():
+    import ctypes as C
+    from tape_amd import _lib
+    if _lib.device_count() > 0:
+        pytest.skip("device present")
+    c = C.c_void_p()
+    assert _lib.lib.te_clay_new(20, 7, 16, C.byref(c)) == 0
+    cfg = _lib.te_slicer_cfg()
+    obj = _lib.te_recover_object(0, 715_048, 0xFFFFE, 0, 0)
+    meta = (C.c_uint8 * 48)()
+    r = _lib.lib.te_recover_batch_device(c, C.byref(cfg), C.c_void_p(16), C.byref(obj), meta, 1, C.c_void_p(16), None)
+    assert r == _lib.TE_ERR_NO_DEVICE
+    _lib.lib.te_clay_free(c)
