@@ -588,6 +588,28 @@ hipError_t launch_meta(const MetaJob *jobs, uint32_t njobs, uint32_t n, hipStrea
     return hipGetLastError();
 }
 
+// Batched device copy (te_recover_batch_device's lost-slice gather): job j's len bytes, 8-byte
+// granules, kCopySplit workgroups per job so one launch replaces a memcpy per object.
+constexpr uint32_t kCopySplit = 32;
+__global__ void __launch_bounds__(256) copy_kernel(const CopyJob *__restrict__ jobs) {
+    const CopyJob J = jobs[blockIdx.x / kCopySplit];
+    const uint32_t part = blockIdx.x % kCopySplit;
+    const uint64_t words = J.len / 8u, per = (words + kCopySplit - 1) / kCopySplit;
+    const uint64_t w0 = part * per, w1 = w0 + per < words ? w0 + per : words;
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(J.src);
+    uint64_t *dst = reinterpret_cast<uint64_t *>(J.dst);
+    for (uint64_t w = w0 + threadIdx.x; w < w1; w += 256u) dst[w] = src[w];
+    if (part == kCopySplit - 1)
+        for (uint64_t b = words * 8u + threadIdx.x; b < J.len; b += 256u) J.dst[b] = J.src[b];
+}
+
+hipError_t launch_copy(const CopyJob *jobs, uint32_t njobs, hipStream_t s) {
+    if (!njobs) return hipSuccess;
+    if ((uint64_t)njobs * kCopySplit > 0x7fffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(copy_kernel, dim3(njobs * kCopySplit), dim3(256), 0, s, jobs);
+    return hipGetLastError();
+}
+
 bool encode_rows_supported(int n, int k, int d) { return n == 20 && d == k + 9 && (k == 7 || k == 10); }
 
 size_t encode_rows_scratch_bytes(const EncArgs &a) {

@@ -220,7 +220,7 @@ struct te_clay {
     std::mutex mu;
     int device = 0;
     hipStream_t stream = nullptr;  // for the synchronous host-buffer entry points
-    Arena enc, dec, rep;
+    Arena enc, dec, rep, rec;
     DevBuf io_in, io_out;          // staging for host-buffer entry points
     DevBuf rec_blob, rec_slices;   // te_recover_batch_device: decoded objects, re-encoded slices
     // te_encode_batch_host pipeline: kPipe slots, each with its own stream, descriptor arena
@@ -334,8 +334,11 @@ void te_clay_free(te_clay *c) {
         c->enc.release();
         c->dec.release();
         c->rep.release();
+        c->rec.release();
         c->io_in.release();
         c->io_out.release();
+        c->rec_blob.release();
+        c->rec_slices.release();
         if (c->stream) (void)hipStreamDestroy(c->stream);
         for (auto &sl : c->pipe) {
             if (sl.s) (void)hipStreamSynchronize(sl.s);
@@ -1083,6 +1086,23 @@ int te_recover_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t 
     if (r) return r;
     r = encode_enqueue(c, cfg, c->rec_blob.as<uint8_t>(), enc.data(), nobj, c->rec_slices.as<uint8_t>(), s, false);
     if (r) return r;
+    // the lost slices out of the re-encoded objects: one gather launch (8-byte aligned: slice
+    // lengths are multiples of 8) or a copy per object otherwise
+    bool aligned = ((uintptr_t)d_out & 7) == 0;
+    for (size_t i = 0; i < nobj; i++) aligned = aligned && (objs[i].out_off & 7) == 0 && (objs[i].slice_len & 7) == 0;
+    if (aligned) {
+        std::vector<CopyJob> jobs(nobj);
+        for (size_t i = 0; i < nobj; i++)
+            jobs[i] = CopyJob{c->rec_slices.as<uint8_t>() + enc[i].out_off + (uint64_t)objs[i].lost * objs[i].slice_len,
+                              d_out + objs[i].out_off, objs[i].slice_len};
+        Arena &A = c->rec;
+        A.img.clear();
+        const size_t off = A.put(jobs.data(), jobs.size() * sizeof(CopyJob));
+        r = A.upload(s);
+        if (r) return r;
+        TE_HIP(launch_copy(A.at<CopyJob>(off), (uint32_t)nobj, s));
+        return A.mark_done(s);
+    }
     for (size_t i = 0; i < nobj; i++)
         TE_HIP(hipMemcpyAsync(d_out + objs[i].out_off,
                               c->rec_slices.as<uint8_t>() + enc[i].out_off + (uint64_t)objs[i].lost * objs[i].slice_len,

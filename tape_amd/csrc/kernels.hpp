@@ -201,6 +201,12 @@ hipError_t launch_commit(const CommitArgs &a, hipStream_t s);
 
 hipError_t launch_encode_rows(int k, bool masked, const EncArgs &a, hipStream_t s);
 hipError_t launch_meta(const MetaJob *jobs, uint32_t njobs, uint32_t n, hipStream_t s);
+struct CopyJob {
+    const uint8_t *src;    // 8-byte aligned
+    uint8_t *dst;          // 8-byte aligned
+    uint64_t len;
+};
+hipError_t launch_copy(const CopyJob *jobs, uint32_t njobs, hipStream_t s);
 hipError_t launch_gpe(const GpeArgs &a, uint32_t max_erased, hipStream_t s);
 hipError_t launch_repair(const RepArgs &a, uint32_t max_erased, hipStream_t s);
 hipError_t launch_repair_stage(RepArgs a, hipStream_t s);
