@@ -104,10 +104,12 @@ def main():
     ap.add_argument("--object-bytes", type=int, default=4 * MiB)
     ap.add_argument("--mode", choices=["encode", "repair", "decode", "commit", "recover"], default="encode")
     ap.add_argument("--cpu-sample", type=int, default=96, help="objects in the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity cores)")
-    ap.add_argument("--copy-objects", type=int, default=256,
-                    help="objects in the copy-inclusive (pinned host -> host) leg, encode mode (0 = skip)")
-    ap.add_argument("--copy-steps", type=int, default=4)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = min(16, affinity cores): the GPU box grants 16 host cores per GPU (pool rules)")
+    ap.add_argument("--copy-objects", type=int, default=-1,
+                    help="objects in the copy-inclusive (pinned host -> host) leg, encode mode "
+                         "(-1 = the whole per-GPU share, 0 = skip)")
+    ap.add_argument("--copy-steps", type=int, default=2)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -246,7 +248,7 @@ def main():
                 ok = ok and lv[j * 32:(j + 1) * 32] == hashlib.sha256(b"LEAF" + sl).digest()
         verified = ok
     copy_inc = None
-    if args.mode == "encode" and args.copy_objects > 0:
+    if args.mode == "encode" and args.copy_objects != 0:
         copy_inc = copy_inclusive(args, torch, dist, world, slicer, batch, d_in, d_out, per, L, dev)
 
     cpu = None
@@ -323,11 +325,11 @@ def copy_inclusive(args, torch, dist, world, slicer, batch, d_in, d_out, per, L,
     slices out, through te_encode_batch_host (3-slot H2D / kernel / D2H pipeline).  Reported
     beside `value`, never as it.  Every rank runs it at once (max over ranks), so at N>1 it
     includes the host-memory / PCIe contention of the node."""
-    m = min(args.copy_objects, args.objects)
+    m = args.objects if args.copy_objects < 0 else min(args.copy_objects, args.objects)
     h_in = torch.empty(m * L, dtype=torch.uint8).pin_memory()
     h_in.copy_(d_in[:m * L])
     h_out = torch.empty(m * per, dtype=torch.uint8).pin_memory()
-    objs = [(i * L, L, i * per, 0) for i in range(m)]
+    objs = batch.encode_descs([(i * L, L, i * per, 0) for i in range(m)])
     batch.encode_batch_host(slicer, h_in, objs, h_out)  # warm-up (pipeline buffers)
     if world > 1:
         dist.barrier()
@@ -336,11 +338,28 @@ def copy_inclusive(args, torch, dist, world, slicer, batch, d_in, d_out, per, L,
         batch.encode_batch_host(slicer, h_in, objs, h_out)
     el = time.perf_counter() - t
     el = max_over_ranks(torch, dist, world, el, dev)
-    ok = bool(torch.equal(h_out[:per], d_out[:per].cpu()))  # same bytes as the device-resident run
+    # same bytes as the device-resident run: first and last object
+    ok = bool(torch.equal(h_out[:per], d_out[:per].cpu()) and
+              torch.equal(h_out[(m - 1) * per:m * per], d_out[(m - 1) * per:m * per].cpu()))
+    # the PCIe legs alone (whole share, pinned, one DMA each way): what bounds the pipeline
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    d_in[:m * L].copy_(h_in, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = m * L / (time.perf_counter() - t) / 1e9
+    t = time.perf_counter()
+    h_out.copy_(d_out[:m * per], non_blocking=True)
+    torch.cuda.synchronize()
+    d2h = m * per / (time.perf_counter() - t) / 1e9
     return {"value": round(m * world * args.copy_steps * L / el / 2**30, 3), "unit": "GiB/s",
             "objects_per_gpu": m, "steps": args.copy_steps, "pinned": True,
             "ms_per_step": round(el / args.copy_steps * 1e3, 3),
-            "h2d_plus_d2h_bytes_per_object": L + per, "matches_device_resident": ok}
+            "h2d_bytes_per_object": L, "d2h_bytes_per_object": per,
+            "h2d_GBps": round(h2d, 2), "d2h_GBps": round(d2h, 2),
+            # PCIe ceilings: both directions at once (full duplex) / one after the other
+            "pcie_duplex_bound_GiBps": round(min(h2d * 1e9 / L, d2h * 1e9 / per) * L / 2**30, 3),
+            "pcie_serial_bound_GiBps": round(m * L / (m * L / (h2d * 1e9) + m * per / (d2h * 1e9)) / 2**30, 3),
+            "matches_device_resident": ok}
 
 
 def cpu_baseline(args, np, torch, d_in, d_out, per, L):
@@ -351,7 +370,7 @@ def cpu_baseline(args, np, torch, d_in, d_out, per, L):
         cores = len(os.sched_getaffinity(0))
     except Exception:
         cores = os.cpu_count() or 1
-    thr = args.cpu_threads or max(1, min(16, cores))
+    thr = args.cpu_threads or max(1, min(16, cores))  # the box's CPU share per GPU is 16 cores
     m = min(args.cpu_sample, args.objects)
     host_in = d_in[:m * L].cpu().numpy()
     clay = O.OracleClay(20, 7, 16)
@@ -366,7 +385,9 @@ def cpu_baseline(args, np, torch, d_in, d_out, per, L):
     O.slicer_encode_np(clay, one)
     single = time.perf_counter() - t
     return {"value": round(m * L / wall / 2**30, 4), "unit": "GiB/s", "cores": thr, "kind": "port",
-            "sample": f"{m} x 4 MiB objects (first {m} of the batch), {thr} threads, one object per thread",
+            "sample": f"{m} x 4 MiB objects (first {m} of the batch), {thr} threads, one object per thread; "
+                      "oracle/clay_oracle.c: per-byte GF(2^8) table lookups, the shape of reed-solomon-erasure's "
+                      "pure-Rust mul_slice",
             "single_thread_GiBps": round(L / single / 2**30, 4), "affinity_cores": cores,
             "gpu_matches_oracle_on_sample": match}
 

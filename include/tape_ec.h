@@ -64,7 +64,8 @@ typedef enum te_status {
 const char *te_strerror(int status);
 /* Number of usable gfx950 devices (0 on a CPU-only host).  Does not create a context. */
 int te_device_count(void);
-/* Bind the calling thread's engine context to a HIP device (default 0). */
+/* Make `device` the calling thread's current HIP device (hipSetDevice).  Handles do not depend on
+ * it: a te_clay runs on the device it is bound to (te_clay_bind_device). */
 int te_set_device(int device);
 /* Detail of the last TE_ERR_HIP/OOM/NO_DEVICE on the calling thread (HIP error string). */
 const char *te_last_error_detail(void);
@@ -94,6 +95,12 @@ int te_clay_new(uint32_t n, uint32_t k, uint32_t d, te_clay **out);
 /* ClayCoder::from_params(ClayParams)  clay.rs:37-39 (packed n | k<<8 | d<<16, encoding.rs:193-197) */
 int te_clay_from_params(uint64_t packed_params, te_clay **out);
 void te_clay_free(te_clay *c);
+/* Device binding (SURVEY 8b device-mask context; one SDK process may drive several GPUs): a handle
+ * is bound to the device that was current on the creating thread; every allocation and launch it
+ * makes runs on that device whatever the calling thread's current device is (the thread's device
+ * is restored on return).  Re-binding drains and frees the handle's device state first. */
+int te_clay_bind_device(te_clay *c, int device);
+int te_clay_device(const te_clay *c);
 int te_clay_get_info(const te_clay *c, te_clay_info *out);
 /* ClayCoder::chunk_size_for  clay.rs:61-73 */
 size_t te_clay_chunk_size_for(const te_clay *c, size_t input_len);
@@ -209,6 +216,12 @@ int te_encode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *
  * should be pinned (hipHostMalloc / hipHostRegister) for full PCIe rate.  Synchronous. */
 int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data,
                          const te_object *objs, size_t nobj, uint8_t *h_out, size_t window_bytes);
+/* The same over several handles (typically one per device): objects are split into contiguous
+ * ranges by bytes, one host thread per handle, each running te_encode_batch_host on its range.
+ * The first error (by handle order) is returned.  Synchronous. */
+int te_encode_batch_host_multi(te_clay *const *coders, size_t ncoders, const te_slicer_cfg *cfg,
+                               const uint8_t *h_data, const te_object *objs, size_t nobj, uint8_t *h_out,
+                               size_t window_bytes);
 
 typedef struct te_decode_object {
     uint64_t slices_off;  /* slice i at d_slices + slices_off + i*slice_len */

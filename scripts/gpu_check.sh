@@ -1,9 +1,9 @@
+#!/bin/bash
+# GPU parity suite (verbose, per-test timeout), then the default bench line.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-rocminfo 2>/dev/null | grep -m1 gfx > gpurun_out/arch.txt
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
-timeout -k 10 400 python bench.py --steps 5 --warmup 2 --cpu-sample 32 > gpurun_out/bench1.log 2>&1
+mkdir -p gpurun_out/check
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/check/pytest_gpu.log 2>&1
+rc=$?; tail -3 gpurun_out/check/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python bench.py > gpurun_out/check/bench.json 2> gpurun_out/check/bench.err || exit $?
+cat gpurun_out/check/bench.json

@@ -1,26 +1,16 @@
 #!/bin/bash
-# PMC passes over the encode-kernel microbenchmark (one launch + 5 timed).  Summary in gpurun_out/pmck/summary.txt
+# PMC passes over the encode microbench (one counter group per pass, each under its own limit).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/pmck
 mkdir -p $OUT
+KB=${KB:-./scripts/kbench}
+rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 i=0
-for C in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
-         "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_ANY SQ_INST_CYCLES_VMEM_WR SQ_LDS_BANK_CONFLICT" \
-         "SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_VMEM_WR_TA_DATA_FIFO_FULL SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM GRBM_GUI_ACTIVE GRBM_COUNT"; do
+for grp in "$@"; do
   i=$((i+1))
-  timeout -k 10 120 rocprofv3 --pmc $C --output-format csv -d $OUT/p$i -o run -- ./scripts/kbench 1024 > $OUT/p$i.log 2>&1 || exit $?
+  timeout -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- $KB 1024 r q > $OUT/p$i.log 2>&1 || exit $?
 done
-python3 - <<'PY' > $OUT/summary.txt
-import csv, glob
-agg = {}
-for cf in glob.glob("gpurun_out/pmck/**/*counter_collection.csv", recursive=True):
-    for r in csv.DictReader(open(cf)):
-        k = r.get("Kernel_Name", "")
-        if "enc_stage" not in k: continue
-        a = agg.setdefault(r["Counter_Name"], [0.0, 0]); a[0] += float(r["Counter_Value"]); a[1] += 1
-for c, (v, n) in sorted(agg.items()):
-    print(f"{c:32s} {v / n:18.1f}   (n={n})")
-PY
-find $OUT -name "*.csv" -size +1M -delete
+python3 scripts/pmc_sum.py $OUT > $OUT/summary.txt 2>&1
+find $OUT -name "*.csv" -size +4M -delete

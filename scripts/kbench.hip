@@ -2,8 +2,11 @@
 // Times enc_stage_kernel<7> over a device-resident 1024 x 4 MiB batch and
 // times each with hipEvents.  hipcc --offload-arch=gfx950 -O3 -std=c++20 -I tape_amd/csrc
 #include "../tape_amd/csrc/encode_stage.hip"
+#include "../tape_amd/csrc/encode_dma.hip"
 #include <cstdio>
 #include <vector>
+#include <map>
+#include <algorithm>
 using namespace tec;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
@@ -17,13 +20,20 @@ __global__ void fill_random(uint32_t *p, size_t n) {
     }
 }
 
+static bool g_dma = true;
+static hipError_t launch_one(const EncArgs &a) { return g_dma ? launch_encode_dma(false, a, 0) : launch_stage<7, false>(a, 0); }
+__global__ void diff_kernel(const uint32_t *x, const uint32_t *y, size_t n, unsigned long long *cnt) {
+    unsigned long long c = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) c += x[i] != y[i];
+    if (c) atomicAdd(cnt, c);
+}
 template <int MODE>
 float run(const EncArgs &a, uint32_t, int reps) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
-    if (launch_stage<7, false>(a, 0) != hipSuccess) printf("launch failed\n");
+    if (launch_one(a) != hipSuccess) printf("launch failed\n");
     (void)hipEventRecord(e0, 0);
-    for (int r = 0; r < reps; r++) (void)launch_stage<7, false>(a, 0);
+    for (int r = 0; r < reps; r++) (void)launch_one(a);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms = 0;
@@ -62,10 +72,56 @@ int main(int argc, char **argv) {
     const double alg = (double)nobj * (L + 20.0 * slen);
     const int reps = 5;
     float t;
+    if (argc > 4 && argv[4][0] == 's') g_dma = false;
+    {
+        int nb_dma = -1, nb_stage = -1;
+        (void)hipFuncSetAttribute((const void *)dma::enc_dma_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dma::kLdsBytes);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_dma, dma::enc_dma_kernel<false>, dma::G * 64, dma::kLdsBytes);
+        (void)hipFuncSetAttribute((const void *)stage::enc_stage_kernel<7, 6, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)stage::lds_bytes(6));
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_stage, stage::enc_stage_kernel<7, 6, false>, 384, stage::lds_bytes(6));
+        printf("occupancy: dma %d WG/CU (lds %u), stage %d WG/CU (lds %zu)\n", nb_dma, dma::kLdsBytes, nb_stage, stage::lds_bytes(6));
+    }
+    if (argc > 3 && argv[3][0] == 'c') {  // check: dma kernel output == stage kernel output
+        uint8_t *ref;
+        const size_t outb = (size_t)nobj * 20 * slen;
+        CK(hipMalloc(&ref, outb));
+        CK(hipMemset(dout, 0, outb));
+        CK(hipMemset(ref, 0, outb));
+        CK((launch_stage<7, false>(a, 0)));
+        CK(hipMemcpy(ref, dout, outb, hipMemcpyDeviceToDevice));
+        CK(hipMemset(dout, 0, outb));
+        CK(launch_encode_dma(false, a, 0));
+        unsigned long long *cnt;
+        CK(hipMalloc(&cnt, 8));
+        CK(hipMemset(cnt, 0, 8));
+        hipLaunchKernelGGL(diff_kernel, dim3(4096), dim3(256), 0, 0, (const uint32_t *)ref, (const uint32_t *)dout, outb / 4, cnt);
+        unsigned long long h = 0;
+        CK(hipMemcpy(&h, cnt, 8, hipMemcpyDeviceToHost));
+        printf("check: dma vs stage differing words %llu of %zu\n", h, outb / 4);
+        return h != 0;
+    }
+#ifdef TEC_DMA_CENSUS
+    if (argc > 3 && argv[3][0] == 'o') {  // residency census of the DMA kernel
+        CK(launch_encode_dma(false, a, 0));
+        CK(hipDeviceSynchronize());
+        std::vector<uint64_t> rec(3 * a.njobs);
+        CK(hipMemcpy(rec.data(), a.scratch, rec.size() * 8, hipMemcpyDeviceToHost));
+        // max concurrent workgroups per CU
+        std::map<uint64_t, std::vector<std::pair<uint64_t, int>>> ev;
+        for (uint32_t i = 0; i < a.njobs; i++) { ev[rec[3 * i]].push_back({rec[3 * i + 1], 1}); ev[rec[3 * i]].push_back({rec[3 * i + 2], -1}); }
+        int maxc = 0; std::map<int, int> hist;
+        for (auto &kv : ev) { auto v = kv.second; std::sort(v.begin(), v.end(), [](auto x, auto y) { return x.first < y.first || (x.first == y.first && x.second < y.second); });
+            int c = 0, m = 0; for (auto &e : v) { c += e.second; m = std::max(m, c); } hist[m]++; maxc = std::max(maxc, m); }
+        printf("census: %zu CUs used, max concurrent WGs per CU %d; histogram:", ev.size(), maxc);
+        for (auto &h : hist) printf(" %d:%d", h.first, h.second);
+        printf("\n");
+        return 0;
+    }
+#endif
     if (argc > 3 && argv[3][0] == 'q') {  // quick: mode 0 only, best of 3
         float best = 1e9f;
         for (int i = 0; i < 5; i++) best = std::min(best, run<0>(a, blocks, 20));
-        printf("mode0 full (best of 5x20) %8.3f ms  %7.1f GB/s\n", best, alg / best / 1e6);
+        printf("%s full (best of 5x20) %8.3f ms  %7.1f GB/s\n", g_dma ? "dma  " : "stage", best, alg / best / 1e6);
         return 0;
     }
     t = run<0>(a, blocks, reps); printf("mode0 full            %8.3f ms  %7.1f GB/s\n", t, alg / t / 1e6);

@@ -104,6 +104,8 @@ def _load() -> C.CDLL:
         "te_strerror": (C.c_char_p, [i]),
         "te_device_count": (i, []),
         "te_set_device": (i, [i]),
+        "te_clay_bind_device": (i, [vp, i]),
+        "te_clay_device": (i, [vp]),
         "te_version": (C.c_char_p, []),
         "te_kernel_timing": (C.c_int, [C.c_int]),
         "te_kernel_time_ms": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),
@@ -137,6 +139,8 @@ def _load() -> C.CDLL:
         "te_slicer_repair": (i, [vp, vp, pp, szp, u8p, u8p, sz]),
         "te_encode_batch_device": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz, vp, vp]),
         "te_encode_batch_host": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz, vp, sz]),
+        "te_encode_batch_host_multi": (i, [C.POINTER(vp), sz, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz,
+                                           vp, sz]),
         "te_decode_batch_device": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_decode_object), u8p, sz,
                                        vp, vp]),
         "te_repair_batch_device": (i, [vp, vp, C.POINTER(te_repair_object), sz, vp, vp]),

@@ -9,7 +9,7 @@ import ctypes as C
 
 from . import _lib
 from ._lib import lib
-from .slicer import ClayCoder, RepairPlan, Slicer, _check
+from .slicer import ClayCoder, DecodeError, RepairPlan, Slicer, _check
 
 
 def _stream_ptr(stream) -> C.c_void_p:
@@ -44,6 +44,18 @@ def encode_batch_host(slicer: Slicer, data, objs: list[tuple[int, int, int, int]
     cfg = slicer._cfg()
     r = lib.te_encode_batch_host(slicer.coder.handle, C.byref(cfg), C.c_void_p(_host_ptr(data)), arr, len(arr),
                                  C.c_void_p(_host_ptr(out)), window_bytes)
+    _check(r, "encode")
+
+
+def encode_batch_host_multi(slicers: list[Slicer], data, objs: list[tuple[int, int, int, int]], out,
+                            window_bytes: int = 0) -> None:
+    """te_encode_batch_host_multi: one host -> host pipeline per handle (typically one handle per
+    device, ClayCoder.bind_device), objects split into contiguous ranges; same profile/config."""
+    arr = objs if _is_desc(objs) else encode_descs(objs)
+    cfg = slicers[0]._cfg()
+    hs = (C.c_void_p * len(slicers))(*[s.coder.handle.value for s in slicers])
+    r = lib.te_encode_batch_host_multi(hs, len(slicers), C.byref(cfg), C.c_void_p(_host_ptr(data)), arr, len(arr),
+                                       C.c_void_p(_host_ptr(out)), window_bytes)
     _check(r, "encode")
 
 
@@ -91,7 +103,7 @@ def recover_batch(slicer: Slicer, slices, objs: list[tuple[int, int, int, int, i
     mb = (C.c_uint8 * max(1, len(metas))).from_buffer_copy(metas if metas else b"\0")
     r = lib.te_recover_batch_device(slicer.coder.handle, C.byref(cfg), C.c_void_p(slices.data_ptr()), arr, mb,
                                     len(arr), C.c_void_p(out.data_ptr()), _stream_ptr(stream))
-    _check(r, "decode")
+    _check(r, "recover")
 
 
 def reconstruct(slicer: Slicer, lost: int, peer_slices: list[tuple[int, bytes]]) -> bytes:
@@ -102,9 +114,16 @@ def reconstruct(slicer: Slicer, lost: int, peer_slices: list[tuple[int, bytes]])
         raise ValueError("no peer slices provided")
     slen = len(peer_slices[0][1])
     n = slicer.coder.n()
+    if not 0 <= lost < n:
+        raise ValueError(f"lost slice {lost} out of range")
     host = bytearray(n * slen)
     mask = 0
     for i, d in peer_slices:
+        # validate_layout (slicer.rs:79-105): every slice the same length, indices in range, once
+        if not 0 <= i < n or mask >> i & 1:
+            raise DecodeError("InvalidLayout")
+        if len(d) != slen:
+            raise DecodeError("InvalidLayout")
         host[i * slen:(i + 1) * slen] = d
         mask |= 1 << i
     dev = torch.frombuffer(host, dtype=torch.uint8).cuda()

@@ -588,25 +588,43 @@ hipError_t launch_meta(const MetaJob *jobs, uint32_t njobs, uint32_t n, hipStrea
     return hipGetLastError();
 }
 
-// Batched device copy (te_recover_batch_device's lost-slice gather): job j's len bytes, 8-byte
-// granules, kCopySplit workgroups per job so one launch replaces a memcpy per object.
-constexpr uint32_t kCopySplit = 32;
-__global__ void __launch_bounds__(256) copy_kernel(const CopyJob *__restrict__ jobs) {
-    const CopyJob J = jobs[blockIdx.x / kCopySplit];
-    const uint32_t part = blockIdx.x % kCopySplit;
-    const uint64_t words = J.len / 8u, per = (words + kCopySplit - 1) / kCopySplit;
-    const uint64_t w0 = part * per, w1 = w0 + per < words ? w0 + per : words;
-    const uint64_t *src = reinterpret_cast<const uint64_t *>(J.src);
-    uint64_t *dst = reinterpret_cast<uint64_t *>(J.dst);
-    for (uint64_t w = w0 + threadIdx.x; w < w1; w += 256u) dst[w] = src[w];
-    if (part == kCopySplit - 1)
-        for (uint64_t b = words * 8u + threadIdx.x; b < J.len; b += 256u) J.dst[b] = J.src[b];
+// Batched gather (te_recover_batch_device's lost-slice assembly): job j copies `valid` bytes
+// from src and zero-fills up to `len` at dst; 8-byte granules when src and dst are 8-aligned.
+// kGatherSplit workgroups per job, so one launch replaces a memcpy per chunk.
+constexpr uint32_t kGatherSplit = 8;
+__global__ void __launch_bounds__(256) gather_kernel(const CopyJob *__restrict__ jobs) {
+    const CopyJob J = jobs[blockIdx.x / kGatherSplit];
+    const uint32_t part = blockIdx.x % kGatherSplit;
+    const uint64_t len = J.len, valid = J.valid < J.len ? J.valid : J.len;
+    const bool wide = ((reinterpret_cast<uintptr_t>(J.src) | reinterpret_cast<uintptr_t>(J.dst)) & 7u) == 0;
+    if (wide) {
+        const uint64_t words = len / 8u, per = (words + kGatherSplit - 1) / kGatherSplit;
+        const uint64_t w0 = part * per, w1 = w0 + per < words ? w0 + per : words;
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(J.src);
+        uint64_t *dst = reinterpret_cast<uint64_t *>(J.dst);
+        for (uint64_t w = w0 + threadIdx.x; w < w1; w += 256u) {
+            const uint64_t b = w * 8u;
+            uint64_t v = 0;
+            if (b + 8u <= valid) {
+                v = src[w];
+            } else if (b < valid) {
+                for (uint32_t k = 0; k < (uint32_t)(valid - b); k++) v |= (uint64_t)J.src[b + k] << (8 * k);
+            }
+            dst[w] = v;
+        }
+        if (part == kGatherSplit - 1)
+            for (uint64_t b = words * 8u + threadIdx.x; b < len; b += 256u) J.dst[b] = b < valid ? J.src[b] : 0;
+    } else {
+        const uint64_t per = (len + kGatherSplit - 1) / kGatherSplit;
+        const uint64_t b0 = part * per, b1 = b0 + per < len ? b0 + per : len;
+        for (uint64_t b = b0 + threadIdx.x; b < b1; b += 256u) J.dst[b] = b < valid ? J.src[b] : 0;
+    }
 }
 
-hipError_t launch_copy(const CopyJob *jobs, uint32_t njobs, hipStream_t s) {
+hipError_t launch_gather(const CopyJob *jobs, uint32_t njobs, hipStream_t s) {
     if (!njobs) return hipSuccess;
-    if ((uint64_t)njobs * kCopySplit > 0x7fffffffull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(copy_kernel, dim3(njobs * kCopySplit), dim3(256), 0, s, jobs);
+    if ((uint64_t)njobs * kGatherSplit > 0x7fffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gather_kernel, dim3(njobs * kGatherSplit), dim3(256), 0, s, jobs);
     return hipGetLastError();
 }
 

@@ -2,8 +2,8 @@
 //
 // Host side of the drop-in for lib/slicer: Slicer striping/padding/rotation/metadata
 // (slicer.rs, adaptive.rs, metadata.rs), repair planning (repair.rs), descriptor building and
-// launch orchestration.  All GF(2^8) arithmetic runs in the HIP kernels (encode_rows.hip,
-// gpe.hip); there is no CPU compute fallback -- without a device the compute calls fail with
+// launch orchestration.  All GF(2^8) arithmetic runs in the HIP kernels (encode_dma.hip,
+// encode_stage.hip, decode_stage.hip, repair_stage.hip, gpe.hip); there is no CPU compute fallback -- without a device the compute calls fail with
 // TE_ERR_NO_DEVICE.
 #include <hip/hip_runtime.h>
 #include <string.h>
@@ -13,6 +13,8 @@
 #include <mutex>
 #include <vector>
 #include <algorithm>
+#include <functional>
+#include <thread>
 #include "../../include/tape_ec.h"
 #include "kernels.hpp"
 #include "sha256.hpp"
@@ -27,6 +29,11 @@ namespace {
 constexpr size_t kStripeSizes[3] = {100000, 1000000, 10000000};  // adaptive.rs:15-19
 
 thread_local char g_last_error[256] = "";
+// TEC_ENCODE_KERNEL=stage selects the previous 1 MB-stripe encode kernel (measurement only)
+const bool g_no_dma_encode = [] {
+    const char *e = getenv("TEC_ENCODE_KERNEL");
+    return e && strcmp(e, "stage") == 0;
+}();
 
 int hip_status(hipError_t e) {
     if (e == hipSuccess) return TE_OK;
@@ -54,6 +61,21 @@ int device_count() {
     }
     return g_device_count;
 }
+
+// Runs the enclosed calls on a handle's device, whatever the calling thread's current device
+// is, and restores the thread's device afterwards.
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) err = hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
 
 struct DevBuf {
     void *p = nullptr;
@@ -218,11 +240,16 @@ struct te_clay {
     ClayHost h;
     bool fast_encode = false;
     std::mutex mu;
-    int device = 0;
+    int device = 0;                // every allocation and launch of this handle runs on it
     hipStream_t stream = nullptr;  // for the synchronous host-buffer entry points
     Arena enc, dec, rep, rec;
     DevBuf io_in, io_out;          // staging for host-buffer entry points
-    DevBuf rec_blob, rec_slices;   // te_recover_batch_device: decoded objects, re-encoded slices
+    // te_recover_batch_device workspaces (decoded objects, re-encoded slices); `rec_done` is
+    // recorded after the last launch that reads them, on `rec_stream`
+    DevBuf rec_blob, rec_slices;
+    hipEvent_t rec_done = nullptr;
+    bool rec_pending = false;
+    hipStream_t rec_stream = nullptr;
     // te_encode_batch_host pipeline: kPipe slots, each with its own stream, descriptor arena
     // and device window buffers, so window w+1's H2D overlaps window w's kernel and D2H.
     static constexpr int kPipe = 3;
@@ -232,6 +259,37 @@ struct te_clay {
         DevBuf in, out;
     } pipe[kPipe];
 };
+
+// Drain and free everything a handle holds on its device (on that device).
+static void release_device_state(te_clay *c) {
+    if (device_count() <= 0) return;
+    DeviceGuard dg(c->device);
+    if (dg.err != hipSuccess) return;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->rec_done) (void)hipEventSynchronize(c->rec_done);
+    for (auto &sl : c->pipe)
+        if (sl.s) (void)hipStreamSynchronize(sl.s);
+    c->enc.release();
+    c->dec.release();
+    c->rep.release();
+    c->rec.release();
+    c->io_in.release();
+    c->io_out.release();
+    c->rec_blob.release();
+    c->rec_slices.release();
+    if (c->rec_done) (void)hipEventDestroy(c->rec_done);
+    c->rec_done = nullptr;
+    c->rec_pending = false;
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    c->stream = nullptr;
+    for (auto &sl : c->pipe) {
+        sl.arena.release();
+        sl.in.release();
+        sl.out.release();
+        if (sl.s) (void)hipStreamDestroy(sl.s);
+        sl.s = nullptr;
+    }
+}
 
 struct te_repair_plan {
     uint32_t lost = 0, ns = 0, d = 0, beta = 0, n = 0;
@@ -319,9 +377,25 @@ int te_clay_new(uint32_t n, uint32_t k, uint32_t d, te_clay **out) {
         return r == -1 ? TE_ERR_INVALID_ARG : TE_ERR_UNSUPPORTED;
     }
     c->fast_encode = encode_rows_supported((int)n, (int)k, (int)d);
+    if (device_count() > 0) {  // bound to the creating thread's current device (te_clay_bind_device)
+        int dev = 0;
+        if (hipGetDevice(&dev) == hipSuccess) c->device = dev;
+    }
     *out = c;
     return TE_OK;
 }
+
+int te_clay_bind_device(te_clay *c, int device) {
+    if (!c) return TE_ERR_INVALID_ARG;
+    if (device < 0 || device >= device_count()) return TE_ERR_NO_DEVICE;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (device == c->device) return TE_OK;
+    release_device_state(c);  // buffers and streams live on the old device
+    c->device = device;
+    return TE_OK;
+}
+
+int te_clay_device(const te_clay *c) { return c ? c->device : -1; }
 
 int te_clay_from_params(uint64_t p, te_clay **out) {
     return te_clay_new((uint32_t)(p & 0xFF), (uint32_t)((p >> 8) & 0xFF), (uint32_t)((p >> 16) & 0xFF), out);
@@ -329,25 +403,7 @@ int te_clay_from_params(uint64_t p, te_clay **out) {
 
 void te_clay_free(te_clay *c) {
     if (!c) return;
-    if (device_count() > 0) {
-        if (c->stream) (void)hipStreamSynchronize(c->stream);
-        c->enc.release();
-        c->dec.release();
-        c->rep.release();
-        c->rec.release();
-        c->io_in.release();
-        c->io_out.release();
-        c->rec_blob.release();
-        c->rec_slices.release();
-        if (c->stream) (void)hipStreamDestroy(c->stream);
-        for (auto &sl : c->pipe) {
-            if (sl.s) (void)hipStreamSynchronize(sl.s);
-            sl.arena.release();
-            sl.in.release();
-            sl.out.release();
-            if (sl.s) (void)hipStreamDestroy(sl.s);
-        }
-    }
+    release_device_state(c);
     delete c;
 }
 
@@ -436,9 +492,13 @@ namespace {
 struct GeomKey {
     uint64_t cs, slice_len;
     bool masked;  // stripe data end not dword aligned -> masked kernel variant
+    bool odd;     // stripe data at an odd address: the fast kernels load 4 bytes at 2-aligned
+                  // addresses only (an odd-address dword near the data end reads short through
+                  // the range check), so such stripes take the generic byte-exact kernel
     bool operator<(const GeomKey &o) const {
         if (cs != o.cs) return cs < o.cs;
         if (slice_len != o.slice_len) return slice_len < o.slice_len;
+        if (odd != o.odd) return odd < o.odd;
         return masked < o.masked;
     }
 };
@@ -451,8 +511,13 @@ int ensure_stream(te_clay *c) {
 
 // Enqueue the encode of a batch.  raw = ClayCoder::encode semantics (no slicing/rotation/meta,
 // slices are the n chunks of one padded input).
+// keep(obj, stripe): which stripes to encode (all when empty); with a selector no metadata
+// suffix is written (te_recover_batch_device writes its own).
+using StripeSel = std::function<bool(size_t, size_t)>;
+
 int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, const te_object *objs,
-                   size_t nobj, uint8_t *d_out, hipStream_t s, bool raw, Arena *arena = nullptr) {
+                   size_t nobj, uint8_t *d_out, hipStream_t s, bool raw, Arena *arena = nullptr,
+                   const StripeSel &keep = StripeSel()) {
     const ClayHost &h = c->h;
     const int n = h.n;
     const int rotated = cfg ? cfg->rotated : 0;
@@ -475,6 +540,7 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
         }
         if (cs % (size_t)h.alpha || slice_len > 0xffffffffull || cs > 0xffffffffull) return TE_ERR_TOO_MUCH_DATA;
         for (size_t st = 0; st < ns; st++) {
+            if (keep && !keep(i, st)) continue;
             EncJob j{};
             const uint64_t start = (uint64_t)st * S;
             j.src = d_data + o.data_off + start;
@@ -483,9 +549,10 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
             j.rot = rotated ? (uint32_t)((st * TE_ROTATION_STEP) % n) : 0u;
             j.dst_skew = (uint32_t)(st * cs);
             const bool masked = ((reinterpret_cast<uintptr_t>(j.src) & 3u) + j.src_len) % 4 != 0;
-            groups[GeomKey{cs, slice_len, masked}].push_back(j);
+            const bool odd = (reinterpret_cast<uintptr_t>(j.src) & 1u) != 0;
+            groups[GeomKey{cs, slice_len, masked, odd}].push_back(j);
         }
-        if (!raw) {
+        if (!raw && !keep) {
             MetaJob m{};
             m.dst = d_out + o.out_off + ns * cs;
             m.slice_len = slice_len;
@@ -530,10 +597,15 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
     int r = A.upload(s);
     if (r) return r;
     // one workspace for every fast-path launch of the call (they run in stream order)
-    auto fast_path = [&](const Launch &L) { return c->fast_encode && (uint64_t)n * L.key.slice_len < 0x7fffffffull; };
+    auto fast_path = [&](const Launch &L) {
+        return c->fast_encode && !L.key.odd && (uint64_t)n * L.key.slice_len < 0x7fffffffull;
+    };
+    auto dma_path = [&](const Launch &L) {
+        return fast_path(L) && encode_dma_supported(n, h.k, (uint32_t)(L.key.cs / h.alpha)) && !g_no_dma_encode;
+    };
     size_t scratch_bytes = 0;
     for (const Launch &L : launches) {
-        if (!fast_path(L)) continue;
+        if (!fast_path(L) || dma_path(L)) continue;
         const uint32_t wps = ((uint32_t)(L.key.cs / h.alpha) + 3) / 4;
         EncArgs a{};
         a.njobs = (uint32_t)L.count;
@@ -574,7 +646,16 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
         const uint32_t wps = (sc + 3) / 4;   // words incl. a 2-column tail when sc % 4 == 2
         const uint32_t full = sc / 4;        // full 4-column words
         // fast kernel addresses an object's slices with 31-bit buffer offsets
-        if (fast_path(L)) {
+        if (dma_path(L)) {  // the 1 MB-stripe kernel (encode_dma.hip)
+            EncArgs a{};
+            a.jobs = A.at<EncJob>(L.off);
+            a.njobs = (uint32_t)L.count;
+            a.cs = cs;
+            a.sc = sc;
+            a.slice_len = (uint32_t)L.key.slice_len;
+            a.n = (uint32_t)n;
+            TE_HIP(launch_encode_dma(L.key.masked, a, s));
+        } else if (fast_path(L)) {
             (void)full;
             EncArgs a{};
             a.jobs = A.at<EncJob>(L.off);
@@ -904,6 +985,18 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
     return A.mark_done(s);
 }
 
+// ClayCoder::plan_repair maps every minimum_to_repair failure to RepairError::Clay(e.to_string())
+// (repair.rs:59-62); the detail text goes to te_last_error_detail().
+int clay_plan_error(int r, int lost_shard, size_t navail, int d) {
+    if (r == -1)
+        snprintf(g_last_error, sizeof(g_last_error), "minimum_to_repair: need %d helpers, %zu available (lost shard %d)",
+                 d, navail, lost_shard);
+    else
+        snprintf(g_last_error, sizeof(g_last_error),
+                 "minimum_to_repair: a column-mate of lost shard %d is not available", lost_shard);
+    return TE_ERR_CLAY;
+}
+
 int build_plan(const te_clay *c, int rotated, uint32_t lost, const uint32_t *avail, size_t navail, uint64_t ns,
                uint64_t cs, te_repair_plan **out) {
     const ClayHost &h = c->h;
@@ -922,7 +1015,7 @@ int build_plan(const te_clay *c, int rotated, uint32_t lost, const uint32_t *ava
         }
         std::vector<int> hs;
         const int r = h.min_to_repair(ls, av, hs);
-        if (r) { delete p; return r == -1 ? TE_ERR_NOT_ENOUGH_HELPERS : TE_ERR_CLAY; }
+        if (r) { delete p; return clay_plan_error(r, ls, navail, h.d); }
         const std::vector<int> planes = h.repair_planes(ls);
         p->lost_shard.push_back((uint32_t)ls);
         for (int sh : hs) {
@@ -947,6 +1040,8 @@ int te_encode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *
     if (!c || !cfg || (!objs && nobj)) return TE_ERR_INVALID_ARG;
     if (device_count() <= 0) return TE_ERR_NO_DEVICE;
     std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    TE_HIP(dg.err);
     return encode_enqueue(c, cfg, d_data, objs, nobj, d_out, (hipStream_t)stream, false);
 }
 
@@ -962,6 +1057,8 @@ int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_
         out_bytes[i] = (uint64_t)c->h.n * g.slice_len;
     }
     std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    TE_HIP(dg.err);
     for (auto &sl : c->pipe)
         if (!sl.s) TE_HIP(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
     // Copy runs: consecutive objects contiguous on the host are moved with one DMA.
@@ -982,7 +1079,7 @@ int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_
         size_t j = i;
         uint64_t in_sz = 0, out_sz = 0;
         while (j < nobj && (j == i || in_sz + out_sz + objs[j].blob_len + out_bytes[j] <= window_bytes)) {
-            in_sz += objs[j].blob_len;
+            in_sz += (objs[j].blob_len + 15) & ~15ull;  // device copies 16-byte aligned
             out_sz += out_bytes[j];
             j++;
         }
@@ -996,7 +1093,7 @@ int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_
             local.push_back(te_object{din, objs[o].blob_len, dout, objs[o].chunk_index});
             add_run(hin, objs[o].data_off, din, objs[o].blob_len);
             add_run(hout, objs[o].out_off, dout, out_bytes[o]);
-            din += objs[o].blob_len;
+            din += (objs[o].blob_len + 15) & ~15ull;
             dout += out_bytes[o];
         }
         for (const Run &r : hin)
@@ -1021,6 +1118,37 @@ int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_
     return rc;
 }
 
+int te_encode_batch_host_multi(te_clay *const *coders, size_t ncoders, const te_slicer_cfg *cfg, const uint8_t *h_data,
+                               const te_object *objs, size_t nobj, uint8_t *h_out, size_t window_bytes) {
+    if (!coders || ncoders == 0 || !cfg || (!objs && nobj)) return TE_ERR_INVALID_ARG;
+    for (size_t i = 0; i < ncoders; i++)
+        if (!coders[i]) return TE_ERR_INVALID_ARG;
+    if (ncoders == 1 || nobj <= 1) return te_encode_batch_host(coders[0], cfg, h_data, objs, nobj, h_out, window_bytes);
+    // contiguous ranges of about equal input bytes
+    uint64_t total = 0;
+    for (size_t i = 0; i < nobj; i++) total += objs[i].blob_len + 1;
+    std::vector<size_t> cut(ncoders + 1, nobj);
+    cut[0] = 0;
+    uint64_t acc = 0;
+    size_t part = 1;
+    for (size_t i = 0; i < nobj && part < ncoders; i++) {
+        acc += objs[i].blob_len + 1;
+        while (part < ncoders && acc * ncoders >= total * part) cut[part++] = i + 1;
+    }
+    std::vector<int> rc(ncoders, TE_OK);
+    std::vector<std::thread> th;
+    for (size_t p = 0; p < ncoders; p++) {
+        if (cut[p + 1] <= cut[p]) continue;
+        th.emplace_back([&, p] {
+            rc[p] = te_encode_batch_host(coders[p], cfg, h_data, objs + cut[p], cut[p + 1] - cut[p], h_out, window_bytes);
+        });
+    }
+    for (auto &t : th) t.join();
+    for (int r : rc)
+        if (r) return r;
+    return TE_OK;
+}
+
 int te_decode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices, const te_decode_object *objs,
                            const uint8_t *h_meta, size_t nobj, uint8_t *d_out, void *stream) {
     if (!c || !cfg || (!objs && nobj) || (!h_meta && nobj)) return TE_ERR_INVALID_ARG;
@@ -1033,6 +1161,8 @@ int te_decode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *
         items[i].out_off = objs[i].out_off;
     }
     std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    TE_HIP(dg.err);
     return decode_enqueue(c, cfg, d_slices, items.data(), items.size(), d_out, (hipStream_t)stream, false);
 }
 
@@ -1047,22 +1177,29 @@ int te_repair_batch_device(te_clay *c, const uint8_t *d_helpers, const te_repair
         items[i] = RepItem{objs[i].plan, objs[i].helper_off, objs[i].out_off, objs[i].metadata};
     }
     std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    TE_HIP(dg.err);
     return repair_enqueue(c, d_helpers, items.data(), items.size(), d_out, (hipStream_t)stream);
 }
 
 // Node recover (network/node/src/features/spool/recover.rs:411-442 `reconstruct`): decode the
-// object from >= k peer slices, re-encode it, keep the lost slice.  Decode and encode run back to
-// back on the stream through device workspaces; only the lost slice leaves them.
+// object from >= k peer slices, re-encode it, keep the lost slice.  Per stripe the lost slice
+// holds one shard (rotation): a data shard is a piece of the decoded object (zero-padded like
+// Slicer::encode's stripe, slicer.rs:276-283), so only stripes whose lost shard is a parity
+// shard are re-encoded.  Objects go through the device workspaces in windows (bounded memory);
+// the workspaces are ordered against a previous call on another stream by `rec_done`.
 int te_recover_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices,
                             const te_recover_object *objs, const uint8_t *h_meta, size_t nobj, uint8_t *d_out,
                             void *stream) {
     if (!c || !cfg || (!objs && nobj) || (!h_meta && nobj)) return TE_ERR_INVALID_ARG;
     if (nobj == 0) return TE_OK;
     if (device_count() <= 0) return TE_ERR_NO_DEVICE;
-    const uint32_t n = (uint32_t)c->h.n;
+    const ClayHost &h = c->h;
+    const uint32_t n = (uint32_t)h.n;
+    const int rotated = cfg->rotated;
     std::vector<DecItem> items(nobj);
     std::vector<te_object> enc(nobj);
-    uint64_t blob_total = 0, slice_total = 0;
+    std::vector<uint64_t> stripe(nobj), nstripes(nobj), chunk(nobj), meta_w(nobj * 6);
     for (size_t i = 0; i < nobj; i++) {
         if (objs[i].lost >= n) return TE_ERR_INVALID_SLICE;
         int r = decode_validate(c, h_meta + i * TE_META_SIZE, objs[i].slice_len, objs[i].avail_mask, items[i]);
@@ -1073,41 +1210,121 @@ int te_recover_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t 
         te_slicer_geometry(c, items[i].blob_len, &g);
         if (g.slice_len != objs[i].slice_len) return TE_ERR_INVALID_LAYOUT;
         items[i].in_base = objs[i].slices_off;
-        items[i].out_off = blob_total;
-        enc[i] = te_object{blob_total, items[i].blob_len, slice_total, m.chunk_index};
-        blob_total += (items[i].blob_len + 15) & ~15ull;
-        slice_total += (uint64_t)n * g.slice_len;
+        enc[i] = te_object{0, items[i].blob_len, 0, m.chunk_index};
+        stripe[i] = g.stripe_size;
+        nstripes[i] = g.num_stripes;  // an empty blob still has one (all-zero) stripe
+        chunk[i] = g.chunk_size;
+        for (int w = 0; w < 6; w++) meta_w[i * 6 + w] = get_u64(h_meta + i * TE_META_SIZE + 8 * w);
+    }
+    auto is_parity = [&](size_t i, size_t st) {
+        return te_slice_to_shard(rotated, n, (uint32_t)st, objs[i].lost) >= (uint32_t)h.k;
+    };
+    // windows: <= kWinBlob decoded bytes and <= kWinSlices re-encoded slice bytes
+    uint64_t kWinBlob = 1ull << 30, kWinSlices = 3ull << 30;
+    if (const char *e = getenv("TEC_RECOVER_WINDOW_BYTES")) {  // tests: force several windows
+        const uint64_t v = strtoull(e, nullptr, 10);
+        if (v) kWinBlob = kWinSlices = v;
+    }
+    struct Win { size_t b, e; uint64_t blob, slices; };
+    std::vector<Win> wins;
+    uint64_t max_blob = 16, max_slices = 16;
+    for (size_t i = 0; i < nobj;) {
+        Win w{i, i, 0, 0};
+        while (w.e < nobj) {
+            const uint64_t bb = (items[w.e].blob_len + 15) & ~15ull, sb = (uint64_t)n * objs[w.e].slice_len;
+            if (w.e > w.b && (w.blob + bb > kWinBlob || w.slices + sb > kWinSlices)) break;
+            w.blob += bb;
+            w.slices += sb;
+            w.e++;
+        }
+        max_blob = std::max(max_blob, w.blob + 16);
+        max_slices = std::max(max_slices, w.slices + 16);
+        wins.push_back(w);
+        i = w.e;
     }
     std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    TE_HIP(dg.err);
     hipStream_t s = (hipStream_t)stream;
-    TE_HIP(c->rec_blob.ensure(blob_total + 16));
-    TE_HIP(c->rec_slices.ensure(slice_total + 16));
-    int r = decode_enqueue(c, cfg, d_slices, items.data(), nobj, c->rec_blob.as<uint8_t>(), s, false);
-    if (r) return r;
-    r = encode_enqueue(c, cfg, c->rec_blob.as<uint8_t>(), enc.data(), nobj, c->rec_slices.as<uint8_t>(), s, false);
-    if (r) return r;
-    // the lost slices out of the re-encoded objects: one gather launch (8-byte aligned: slice
-    // lengths are multiples of 8) or a copy per object otherwise
-    bool aligned = ((uintptr_t)d_out & 7) == 0;
-    for (size_t i = 0; i < nobj; i++) aligned = aligned && (objs[i].out_off & 7) == 0 && (objs[i].slice_len & 7) == 0;
-    if (aligned) {
-        std::vector<CopyJob> jobs(nobj);
-        for (size_t i = 0; i < nobj; i++)
-            jobs[i] = CopyJob{c->rec_slices.as<uint8_t>() + enc[i].out_off + (uint64_t)objs[i].lost * objs[i].slice_len,
-                              d_out + objs[i].out_off, objs[i].slice_len};
+    if (!c->rec_done) TE_HIP(hipEventCreateWithFlags(&c->rec_done, hipEventDisableTiming));
+    if (max_blob > c->rec_blob.cap || max_slices > c->rec_slices.cap) {
+        if (c->rec_pending) TE_HIP(hipEventSynchronize(c->rec_done));  // queued work may still use them
+    } else if (c->rec_pending && c->rec_stream != s) {
+        TE_HIP(hipStreamWaitEvent(s, c->rec_done, 0));
+    }
+    TE_HIP(c->rec_blob.ensure(max_blob));
+    TE_HIP(c->rec_slices.ensure(max_slices));
+    uint8_t *const blob = c->rec_blob.as<uint8_t>(), *const slices = c->rec_slices.as<uint8_t>();
+    std::vector<CopyJob> jobs;
+    std::vector<MetaJob> metas;
+    std::vector<te_object> wenc;
+    std::vector<uint64_t> blob_off;
+    int r = TE_OK;
+    for (const Win &w : wins) {
+        blob_off.assign(w.e - w.b, 0);
+        wenc.clear();
+        uint64_t bo = 0, so = 0;
+        for (size_t i = w.b; i < w.e; i++) {
+            items[i].out_off = bo;
+            blob_off[i - w.b] = bo;
+            te_object e = enc[i];
+            e.data_off = bo;
+            e.out_off = so;
+            wenc.push_back(e);
+            bo += (items[i].blob_len + 15) & ~15ull;
+            so += (uint64_t)n * objs[i].slice_len;
+        }
+        if ((r = decode_enqueue(c, cfg, d_slices, items.data() + w.b, w.e - w.b, blob, s, false))) break;
+        bool any_parity = false;
+        for (size_t i = w.b; i < w.e && !any_parity; i++)
+            for (uint64_t st = 0; st < nstripes[i]; st++) any_parity = any_parity || is_parity(i, st);
+        if (any_parity &&
+            (r = encode_enqueue(c, cfg, blob, wenc.data(), wenc.size(), slices, s, false, nullptr,
+                                [&](size_t o, size_t st) { return is_parity(w.b + o, st); })))
+            break;
+        // assemble the lost slices: per stripe the lost shard's chunk, then the suffix
+        jobs.clear();
+        metas.clear();
+        for (size_t i = w.b; i < w.e; i++) {
+            const DecItem &it = items[i];
+            const uint64_t cs = chunk[i], slen = objs[i].slice_len, ns = nstripes[i];
+            uint8_t *dst = d_out + objs[i].out_off;
+            for (uint64_t st = 0; st < ns; st++) {
+                const uint32_t sh = te_slice_to_shard(rotated, n, (uint32_t)st, objs[i].lost);
+                if (sh >= (uint32_t)h.k) {
+                    jobs.push_back(CopyJob{slices + wenc[i - w.b].out_off + (uint64_t)objs[i].lost * slen + st * cs,
+                                           dst + st * cs, cs, cs});
+                } else {
+                    // data shard sh of stripe st: object bytes [st*S + sh*cs, ...) clipped to the
+                    // stripe and the object, zero beyond
+                    const uint64_t start = st * stripe[i] + (uint64_t)sh * cs;
+                    const uint64_t end = std::min<uint64_t>(it.blob_len, (st + 1) * stripe[i]);
+                    const uint64_t valid = start < end ? std::min<uint64_t>(cs, end - start) : 0;
+                    jobs.push_back(CopyJob{blob + blob_off[i - w.b] + std::min(start, it.blob_len), dst + st * cs, cs, valid});
+                }
+            }
+            MetaJob m{};
+            m.dst = dst + ns * cs;
+            m.slice_len = 0;
+            for (int k = 0; k < 6; k++) m.words[k] = meta_w[i * 6 + k];
+            metas.push_back(m);
+        }
         Arena &A = c->rec;
         A.img.clear();
         const size_t off = A.put(jobs.data(), jobs.size() * sizeof(CopyJob));
-        r = A.upload(s);
-        if (r) return r;
-        TE_HIP(launch_copy(A.at<CopyJob>(off), (uint32_t)nobj, s));
-        return A.mark_done(s);
+        const size_t moff = A.put(metas.data(), metas.size() * sizeof(MetaJob));
+        if ((r = A.upload(s))) break;
+        KTimer kt(s);
+        if ((r = hip_status(launch_gather(A.at<CopyJob>(off), (uint32_t)jobs.size(), s)))) break;
+        if ((r = hip_status(launch_meta(A.at<MetaJob>(moff), (uint32_t)metas.size(), 1u, s)))) break;
+        kt.stop();
+        if ((r = A.mark_done(s))) break;
     }
-    for (size_t i = 0; i < nobj; i++)
-        TE_HIP(hipMemcpyAsync(d_out + objs[i].out_off,
-                              c->rec_slices.as<uint8_t>() + enc[i].out_off + (uint64_t)objs[i].lost * objs[i].slice_len,
-                              objs[i].slice_len, hipMemcpyDeviceToDevice, s));
-    return TE_OK;
+    // later calls (any stream) order against everything this one enqueued
+    const int r2 = hip_status(hipEventRecord(c->rec_done, s));
+    c->rec_pending = true;
+    c->rec_stream = s;
+    return r ? r : r2;
 }
 
 int te_slicer_encode(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *data, size_t len, uint8_t *slices,
@@ -1118,6 +1335,8 @@ int te_slicer_encode(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *data, 
     const size_t total = (size_t)c->h.n * g.slice_len;
     if (cap < total) return TE_ERR_BUFFER_TOO_SMALL;
     std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    TE_HIP(dg.err);
     int r = ensure_stream(c);
     if (r) return r;
     TE_HIP(c->io_in.ensure(len + 16));
@@ -1139,6 +1358,8 @@ int te_clay_encode(te_clay *c, const uint8_t *data, size_t len, uint8_t *chunks,
     if (chunk_size) *chunk_size = cs;
     if (cap < total) return TE_ERR_BUFFER_TOO_SMALL;
     std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    TE_HIP(dg.err);
     int r = ensure_stream(c);
     if (r) return r;
     TE_HIP(c->io_in.ensure(len + 16));
@@ -1164,6 +1385,8 @@ int te_clay_decode(te_clay *c, const uint8_t *const *chunks, size_t cs, uint8_t 
     if (cs == 0 || cs % (size_t)h.alpha) return TE_ERR_BAD_ENCODING;
     if (cap < (size_t)h.k * cs) return TE_ERR_BUFFER_TOO_SMALL;
     std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    TE_HIP(dg.err);
     int r = ensure_stream(c);
     if (r) return r;
     const size_t total = (size_t)h.n * cs;
@@ -1199,6 +1422,8 @@ int te_slicer_decode(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *const 
     if (it.blob_len == 0) return TE_OK;
     if (!out || cap < it.blob_len) return TE_ERR_BUFFER_TOO_SMALL;
     std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    TE_HIP(dg.err);
     r = ensure_stream(c);
     if (r) return r;
     const size_t total = (size_t)h.n * slice_len;
@@ -1227,7 +1452,7 @@ int te_clay_plan_repair(const te_clay *c, uint32_t lost, const uint32_t *availab
     if (lost >= (uint32_t)h.n) return TE_ERR_INVALID_SLICE;
     std::vector<int> av(available, available + navail), hs;
     const int r = h.min_to_repair((int)lost, av, hs);
-    if (r) return r == -1 ? TE_ERR_NOT_ENOUGH_HELPERS : TE_ERR_CLAY;
+    if (r) return clay_plan_error(r, (int)lost, navail, h.d);
     if (helpers_out)
         for (size_t i = 0; i < hs.size(); i++) helpers_out[i] = (uint32_t)hs[i];
     if (sub_chunks_out) {
@@ -1330,6 +1555,8 @@ int te_slicer_repair(te_clay *c, const te_repair_plan *p, const uint8_t *const *
         total += (need[sl] + 15) & ~15ull;
     }
     std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    TE_HIP(dg.err);
     int r = ensure_stream(c);
     if (r) return r;
     TE_HIP(c->io_in.ensure(total + 16));
@@ -1351,7 +1578,10 @@ int te_clay_repair(te_clay *c, uint32_t lost, const uint32_t *helpers, const uin
     if (!c || !helpers || !helper_data || !out) return TE_ERR_INVALID_ARG;
     const ClayHost &h = c->h;
     if (lost >= (uint32_t)h.n) return TE_ERR_INVALID_SLICE;
-    if (nhelpers != (size_t)h.d) return TE_ERR_NOT_ENOUGH_HELPERS;
+    if (nhelpers != (size_t)h.d) {  // clay_codes::ClayCode::repair rejects it -> RepairError::Clay (repair.rs:85-87)
+        snprintf(g_last_error, sizeof(g_last_error), "repair: need exactly d=%d helpers, got %zu", h.d, nhelpers);
+        return TE_ERR_CLAY;
+    }
     if (chunk_size == 0 || chunk_size % (size_t)h.alpha) return TE_ERR_INVALID_LAYOUT;
     // one-stripe, identity-mapped plan with the caller's helper set
     te_repair_plan p;

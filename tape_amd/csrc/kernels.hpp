@@ -200,13 +200,17 @@ struct CommitArgs {
 hipError_t launch_commit(const CommitArgs &a, hipStream_t s);
 
 hipError_t launch_encode_rows(int k, bool masked, const EncArgs &a, hipStream_t s);
+// encode_dma.hip: Clay(20,7,16), 1,280 < sub-chunk <= 1,440 bytes (the 1 MB stripes), no scratch
+bool encode_dma_supported(int n, int k, uint32_t sc);
+hipError_t launch_encode_dma(bool masked, const EncArgs &a, hipStream_t s);
 hipError_t launch_meta(const MetaJob *jobs, uint32_t njobs, uint32_t n, hipStream_t s);
 struct CopyJob {
-    const uint8_t *src;    // 8-byte aligned
-    uint8_t *dst;          // 8-byte aligned
-    uint64_t len;
+    const uint8_t *src;
+    uint8_t *dst;
+    uint64_t len;          // bytes written at dst
+    uint64_t valid;        // bytes copied from src; the rest of len is zero-filled
 };
-hipError_t launch_copy(const CopyJob *jobs, uint32_t njobs, hipStream_t s);
+hipError_t launch_gather(const CopyJob *jobs, uint32_t njobs, hipStream_t s);
 hipError_t launch_gpe(const GpeArgs &a, uint32_t max_erased, hipStream_t s);
 hipError_t launch_repair(const RepArgs &a, uint32_t max_erased, hipStream_t s);
 hipError_t launch_repair_stage(RepArgs a, hipStream_t s);

@@ -86,10 +86,20 @@ def _engine_error(code: int) -> EngineError:
 
 
 def _check(code: int, kind: str) -> None:
+    """Raise the reference's error for a status.  kind "recover" (node recover = decode then
+    encode) maps through the decode table, then the encode table."""
     if code == 0:
         return
+    if kind == "recover":
+        if code in _DEC:
+            raise DecodeError(_DEC[code])
+        if code in _ENC:
+            raise EncodeError(_ENC[code])
+        raise _engine_error(code)
     table = {"encode": (_ENC, EncodeError), "decode": (_DEC, DecodeError), "repair": (_REP, RepairError)}[kind]
     if code in table[0]:
+        if kind == "repair" and code == _lib.TE_ERR_CLAY:  # RepairError::Clay(String), repair.rs:59-62
+            raise RepairError("Clay", lib.te_last_error_detail().decode())
         raise table[1](table[0][code])
     raise _engine_error(code)
 
@@ -257,6 +267,15 @@ class ClayCoder:
     def handle(self) -> C.c_void_p:
         return self._h
 
+    def bind_device(self, device: int) -> None:
+        """te_clay_bind_device: run this coder's allocations and launches on `device`."""
+        r = lib.te_clay_bind_device(self._h, device)
+        if r:
+            raise _engine_error(r)
+
+    def device(self) -> int:
+        return int(lib.te_clay_device(self._h))
+
     def k(self) -> int:
         return self._info.k
 
@@ -324,8 +343,6 @@ class ClayCoder:
         ptrs = (C.c_void_p * max(1, len(ids)))(*[C.cast(b, C.c_void_p) for b in keep])
         out = (C.c_uint8 * chunk_size)()
         r = lib.te_clay_repair(self._h, lost, hs, ptrs, len(ids), chunk_size, out)
-        if r == _lib.TE_ERR_NOT_ENOUGH_HELPERS:
-            raise RepairError("Clay", f"need exactly d={self.d()} helpers, got {len(ids)}")
         _check(r, "repair")
         return bytes(out)
 

@@ -121,6 +121,36 @@ def test_plan_repair_clay_level(oracle):
         c.plan_repair(0, list(range(1, 16)))  # d-1 available
 
 
+def test_plan_failures_are_clay_errors():
+    """ClayCoder::plan_repair maps every minimum_to_repair failure to RepairError::Clay(String)
+    (repair.rs:59-62); repair_plan_from_params propagates it (repair.rs:170)."""
+    c = T.ClayCoder(20, 7, 16)
+    with pytest.raises(T.RepairError) as e:
+        c.plan_repair(0, list(range(1, 16)))  # d - 1 available
+    assert e.value.variant == "Clay" and "need 16 helpers" in str(e.value)
+    with pytest.raises(T.RepairError) as e:
+        c.plan_repair(0, [i for i in range(1, N) if i != 3])  # a column-mate of node 0 missing
+    assert e.value.variant == "Clay" and "column-mate" in str(e.value)
+    s = T.Slicer.clay_default()
+    with pytest.raises(T.RepairError) as e:
+        s.repair_plan_from_params(5, list(range(6, 20)), 4 * 1024 * 1024, 1_000_000)
+    assert e.value.variant == "Clay"
+    # repair_full with no helpers stays NotEnoughHelpers (repair.rs:293-296)
+    with pytest.raises(T.RepairError) as e:
+        s.repair_full(0, [])
+    assert e.value.variant == "NotEnoughHelpers"
+
+
+def test_device_binding_without_device():
+    if T.device_count() > 0:
+        pytest.skip("device present")
+    c = T.ClayCoder(20, 7, 16)
+    from tape_amd._lib import lib
+    assert lib.te_clay_device(c.handle) == 0
+    assert lib.te_clay_bind_device(c.handle, 0) == _lib.TE_ERR_NO_DEVICE
+    assert lib.te_clay_bind_device(None, 0) == _lib.TE_ERR_INVALID_ARG
+
+
 def test_extract_repair_data_matches_oracle(oracle):
     o = oracle.OracleClay(20, 7, 16)
     data = oracle.splitmix64_bytes(9, 300_000).tobytes()
