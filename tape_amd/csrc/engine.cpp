@@ -34,6 +34,11 @@ const bool g_no_dma_encode = [] {
     const char *e = getenv("TEC_ENCODE_KERNEL");
     return e && strcmp(e, "stage") == 0;
 }();
+// TEC_REPAIR_KERNEL=stage keeps the folded repair kernel off (measurement / cross-check only)
+const bool g_no_fold_repair = [] {
+    const char *e = getenv("TEC_REPAIR_KERNEL");
+    return e && strcmp(e, "stage") == 0;
+}();
 
 int hip_status(hipError_t e) {
     if (e == hipSuccess) return TE_OK;
@@ -954,27 +959,56 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
     const size_t pool_off = A.put(pool.data(), pool.size() * sizeof(uint16_t));
     const size_t pind_off = A.put(pind.data(), pind.size() * sizeof(uint16_t));
     const size_t meta_off = A.put(metas.data(), metas.size() * sizeof(MetaJob));
-    std::vector<std::pair<uint64_t, size_t>> offs;
-    for (auto &kv : groups) offs.push_back({kv.first, A.put(kv.second.data(), kv.second.size() * sizeof(RepJob))});
+    // stripes whose pattern is the all-available one of Clay(20,7,16) go to the folded kernel
+    // (one launch per lost column), the rest to the staged / generic kernel
+    std::vector<int> fold_col(pats.size(), -1);
+    for (size_t i = 0; i < pats.size() && !g_no_fold_repair; i++)
+        if (h.nu == 0 && h.n == 2 * h.q)
+            fold_col[i] = repair_fold_column(h.q, h.t, h.k, pats[i].beta, 8, pats[i].lost, pats[i].erased_mask,
+                                             pats[i].aloof_mask);
+    struct Launch { uint64_t cs; int fold; size_t off, njobs; };
+    std::vector<Launch> offs;
+    for (auto &kv : groups) {
+        const uint32_t sc = (uint32_t)(kv.first / (uint64_t)h.alpha);
+        std::vector<RepJob> part[3];  // fold column 0, fold column 1, other
+        for (const RepJob &j : kv.second) {
+            const int fc = sc >= 8 ? fold_col[j.pattern] : -1;
+            RepJob jj = j;
+            if (fc >= 0) {  // the folded kernel loads every node unconditionally (repair_fold.hip)
+                jj.aux = pats[j.pattern].lost % (uint32_t)h.q;
+                const uint8_t *any = nullptr;
+                for (int nd = 0; nd < h.qt && !any; nd++) any = jj.helper[nd];
+                for (int nd = 0; nd < h.qt; nd++)
+                    if (!jj.helper[nd]) jj.helper[nd] = any;
+            }
+            part[fc >= 0 ? fc : 2].push_back(jj);
+        }
+        for (int f = 0; f < 3; f++)
+            if (!part[f].empty())
+                offs.push_back({kv.first, f < 2 ? f : -1, A.put(part[f].data(), part[f].size() * sizeof(RepJob)),
+                                part[f].size()});
+    }
     int r = A.upload(s);
     if (r) return r;
     KTimer kt(s);
     if (!metas.empty()) TE_HIP(launch_meta(A.at<MetaJob>(meta_off), (uint32_t)metas.size(), 1u, s));
     for (auto &o : offs) {
-        const uint64_t cs = o.first;
+        const uint64_t cs = o.cs;
         const uint32_t sc = (uint32_t)(cs / (uint64_t)h.alpha);
         const uint32_t wps = sc >= 4 ? (sc + 3) / 4 : 1;
         RepArgs a{};
-        a.jobs = A.at<RepJob>(o.second);
+        a.jobs = A.at<RepJob>(o.off);
         a.patterns = A.at<RepPattern>(pat_off);
         a.plane_pool = A.at<uint16_t>(pool_off);
         a.plane_ind = A.at<uint16_t>(pind_off);
-        a.njobs = (uint32_t)groups[o.first].size();
+        a.njobs = (uint32_t)o.njobs;
         a.words_per_stripe = wps;
         a.groups_per_stripe = (wps + kGpeWords - 1) / kGpeWords;
         a.cs = (uint32_t)cs; a.sc = sc; a.q = h.q; a.t = h.t; a.alpha = h.alpha;
         for (int i = 0; i < 16; i++) a.qpow[i] = h.qpow[i];
-        if (staged && sc >= 8) {  // staged kernel: coalesced loads, whole-row stores
+        if (o.fold >= 0) {
+            TE_HIP(launch_repair_fold(o.fold, a, s));
+        } else if (staged && sc >= 8) {  // staged kernel: coalesced loads, whole-row stores
             a.progs = A.at<RepProg>(prog_off);
             TE_HIP(launch_repair_stage(a, s));
         } else {

@@ -96,7 +96,7 @@ struct RepJob {
     const uint8_t *helper[kMaxNodes];  // per internal node: this stripe's beta sub-chunks (or null)
     uint8_t *out;                      // lost chunk destination (chunk_size bytes)
     uint32_t pattern;
-    uint32_t pad_;
+    uint32_t aux;                      // repair_fold.hip: x of the lost node
 };
 
 // Staged repair kernel (repair_stage.hip): per pattern, the uniform control data of every
@@ -214,6 +214,11 @@ hipError_t launch_gather(const CopyJob *jobs, uint32_t njobs, hipStream_t s);
 hipError_t launch_gpe(const GpeArgs &a, uint32_t max_erased, hipStream_t s);
 hipError_t launch_repair(const RepArgs &a, uint32_t max_erased, hipStream_t s);
 hipError_t launch_repair_stage(RepArgs a, hipStream_t s);
+// repair_fold.hip: Clay(20,7,16) with every other node available (the decoding matrix folded per
+// lost column); repair_fold_column() -> 0/1 for such a pattern, else -1
+int repair_fold_column(uint32_t q, uint32_t t, uint32_t k, uint32_t beta, uint32_t sc, uint32_t lost,
+                       uint64_t erased_mask, uint64_t aloof_mask);
+hipError_t launch_repair_fold(int yl, RepArgs a, hipStream_t s);
 bool repair_stage_supported(uint32_t q, uint32_t beta, uint32_t sc, uint32_t nerased, uint32_t nknown, uint64_t aloof_mask);
 bool encode_rows_supported(int n, int k, int d);
 size_t encode_rows_scratch_bytes(const EncArgs &a);  // a.njobs, a.groups_per_stripe set
