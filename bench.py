@@ -82,6 +82,21 @@ def dist_setup(torch, dist, backend: str):
     return world, rank, local
 
 
+# The kernels one step of each mode runs on the default workload (rocprofv3 names, prefix match).
+# profiles/traffic.json holds per mode the HBM bytes these moved per step, measured by
+# scripts/profile_modes.sh + scripts/traffic.py; it is used only while the names still match.
+KERNELS = {
+    "encode": ["tec::dma::enc_dma_kernel<false>"],
+    "repair": ["tec::rfold::rep_fold_kernel<0, 6>", "tec::rfold::rep_fold_kernel<1, 6>"],
+    "decode": ["tec::dstage::dec_stage_kernel<7, 6>"],
+    "commit": ["tec::leaf_kernel", "tec::tree_kernel"],
+}
+
+
+def kernel_names(mode: str) -> list:
+    return KERNELS.get(mode, [])
+
+
 def rank_objects(rank: int, nobj: int) -> tuple[int, int]:
     """Contiguous global object range [first, first + nobj) of this rank (weak scaling)."""
     return rank * nobj, rank * nobj + nobj
@@ -247,9 +262,22 @@ def main():
                 sl = d_out[i * per + j * g.slice_len:i * per + (j + 1) * g.slice_len].cpu().numpy().tobytes()
                 ok = ok and lv[j * 32:(j + 1) * 32] == hashlib.sha256(b"LEAF" + sl).digest()
         verified = ok
-    copy_inc = None
+    commit_sweep = None
+    if args.mode == "commit":  # leaf-kernel parallelism = slices in the batch: rate against batch size
+        commit_sweep = {}
+        for m in (16, 64, 256, 1024, 2048, 4096):
+            if m > nobj:
+                break
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(3):
+                merkle.commit_batch(d_out, per, g.slice_len, N, m, d_leaf, d_root, d_proof, T.SLICE_TREE_HEIGHT, stream)
+            torch.cuda.synchronize()
+            commit_sweep[str(m)] = round(3 * m * L / (time.perf_counter() - t) / 2**30, 2)
+    copy_inc = copy_commit = None
     if args.mode == "encode" and args.copy_objects != 0:
         copy_inc = copy_inclusive(args, torch, dist, world, slicer, batch, d_in, d_out, per, L, dev)
+        copy_commit = copy_inclusive_commit(args, torch, dist, world, slicer, batch, d_in, d_out, per, L, dev)
 
     cpu = None
     if rank == 0 and args.cpu_sample > 0 and args.mode == "encode":
@@ -259,9 +287,9 @@ def main():
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("mode") == args.mode and tj.get("objects") == nobj:
-                traffic = tj.get("hbm_bytes_per_launch")
+            tj = json.load(open(args.traffic_json)).get(args.mode, {})  # per mode (scripts/traffic.py)
+            if tj.get("objects") == nobj and tj.get("kernels") == kernel_names(args.mode):
+                traffic = tj.get("hbm_bytes_per_step")
         except Exception:
             traffic = None
     if rank == 0:
@@ -295,6 +323,8 @@ def main():
                          "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
             "cpu_baseline": cpu,
             "copy_inclusive": copy_inc,
+            "copy_inclusive_encode_commit": copy_commit,
+            "commit_GiBps_vs_objects": commit_sweep,
             "outputs_verified": verified,
         }
         print(json.dumps(line), flush=True)
@@ -360,6 +390,44 @@ def copy_inclusive(args, torch, dist, world, slicer, batch, d_in, d_out, per, L,
             "pcie_duplex_bound_GiBps": round(min(h2d * 1e9 / L, d2h * 1e9 / per) * L / 2**30, 3),
             "pcie_serial_bound_GiBps": round(m * L / (m * L / (h2d * 1e9) + m * per / (d2h * 1e9)) / 2**30, 3),
             "matches_device_resident": ok}
+
+
+def copy_inclusive_commit(args, torch, dist, world, slicer, batch, d_in, d_out, per, L, dev):
+    """Copy-inclusive encode + commitments (SURVEY 8f-4): BlobEncoder::encode_with_proofs per object
+    (sdk/src/codec/encoder.rs:220-260) as the stream writer runs it (sdk/src/stream/write.rs:
+    332-362), through te_encode_commit_batch_host: pinned object bytes in; slices, leaf hashes,
+    roots and proofs out.  Per window size: the leaf kernel's parallelism is one lane per slice,
+    so larger windows hash more slices at once."""
+    m = args.objects if args.copy_objects < 0 else min(args.copy_objects, args.objects)
+    N, H = 20, 5
+    h_in = torch.empty(m * L, dtype=torch.uint8).pin_memory()
+    h_in.copy_(d_in[:m * L])
+    h_out = torch.empty(m * per, dtype=torch.uint8).pin_memory()
+    leaf = torch.empty(m * N * 32, dtype=torch.uint8).pin_memory()
+    root = torch.empty(m * 32, dtype=torch.uint8).pin_memory()
+    proof = torch.empty(m * N * H * 32, dtype=torch.uint8).pin_memory()
+    objs = batch.encode_descs([(i * L, L, i * per, 0) for i in range(m)])
+    res = {}
+    for wgib in (1, 4):
+        wb = wgib << 30
+        batch.encode_commit_batch_host(slicer, h_in, objs, h_out, leaf, root, proof, window_bytes=wb)  # warm-up
+        if world > 1:
+            dist.barrier()
+        t = time.perf_counter()
+        for _ in range(args.copy_steps):
+            batch.encode_commit_batch_host(slicer, h_in, objs, h_out, leaf, root, proof, window_bytes=wb)
+        el = max_over_ranks(torch, dist, world, time.perf_counter() - t, dev)
+        res[f"window_{wgib}GiB_GiBps"] = round(m * world * args.copy_steps * L / el / 2**30, 3)
+    # the first object's slices and commitments against the device-resident encode + hashlib
+    import hashlib
+    ok = bool(torch.equal(h_out[:per], d_out[:per].cpu()))
+    sl_len = per // N
+    for i in range(N):
+        sl = h_out[i * sl_len:(i + 1) * sl_len].numpy().tobytes()
+        ok = ok and leaf[i * 32:(i + 1) * 32].numpy().tobytes() == hashlib.sha256(b"LEAF" + sl).digest()
+    best = max(res.values())
+    return {"value": best, "unit": "GiB/s", "objects_per_gpu": m, "steps": args.copy_steps, "pinned": True,
+            "tree_height": H, "proofs": True, "by_window": res, "matches_device_resident": ok}
 
 
 def cpu_baseline(args, np, torch, d_in, d_out, per, L):

@@ -222,6 +222,18 @@ int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_
 int te_encode_batch_host_multi(te_clay *const *coders, size_t ncoders, const te_slicer_cfg *cfg,
                                const uint8_t *h_data, const te_object *objs, size_t nobj, uint8_t *h_out,
                                size_t window_bytes);
+/* te_encode_batch_host plus the slice commitments of BlobEncoder::encode_with_proofs
+ * (sdk/src/codec/encoder.rs:220-260; the stream writer's per-chunk step, sdk/src/stream/write.rs:
+ * 332-362): per object o, leaf hashes hash_leaf(slice i) at h_leaf_hashes + (o*n + i)*32, the
+ * root root_from_leaf_hashes::<height> at h_roots + o*32 and, if h_proofs is not NULL, proof i
+ * (create_proof_from_leaf_hashes::<height>) at h_proofs + ((o*n + i)*height + level)*32.
+ * Hashed on the device from each window's slices before they are copied out.  Requires
+ * n <= 2^height, height <= 32 and slice_len % 4 == 0 (every Clay profile with even alpha).
+ * Synchronous; objects keep their order. */
+int te_encode_commit_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data,
+                                const te_object *objs, size_t nobj, uint8_t *h_out, uint32_t height,
+                                uint8_t *h_leaf_hashes, uint8_t *h_roots, uint8_t *h_proofs,
+                                size_t window_bytes);
 
 typedef struct te_decode_object {
     uint64_t slices_off;  /* slice i at d_slices + slices_off + i*slice_len */

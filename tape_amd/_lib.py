@@ -141,6 +141,8 @@ def _load() -> C.CDLL:
         "te_encode_batch_host": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz, vp, sz]),
         "te_encode_batch_host_multi": (i, [C.POINTER(vp), sz, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz,
                                            vp, sz]),
+        "te_encode_commit_batch_host": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz, vp,
+                                            C.c_uint32, vp, vp, vp, sz]),
         "te_decode_batch_device": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_decode_object), u8p, sz,
                                        vp, vp]),
         "te_repair_batch_device": (i, [vp, vp, C.POINTER(te_repair_object), sz, vp, vp]),

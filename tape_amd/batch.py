@@ -9,7 +9,7 @@ import ctypes as C
 
 from . import _lib
 from ._lib import lib
-from .slicer import ClayCoder, DecodeError, RepairPlan, Slicer, _check
+from .slicer import SLICE_TREE_HEIGHT, ClayCoder, DecodeError, RepairPlan, Slicer, _check
 
 
 def _stream_ptr(stream) -> C.c_void_p:
@@ -56,6 +56,21 @@ def encode_batch_host_multi(slicers: list[Slicer], data, objs: list[tuple[int, i
     hs = (C.c_void_p * len(slicers))(*[s.coder.handle.value for s in slicers])
     r = lib.te_encode_batch_host_multi(hs, len(slicers), C.byref(cfg), C.c_void_p(_host_ptr(data)), arr, len(arr),
                                        C.c_void_p(_host_ptr(out)), window_bytes)
+    _check(r, "encode")
+
+
+def encode_commit_batch_host(slicer: Slicer, data, objs: list[tuple[int, int, int, int]], out, leaf_hashes, roots,
+                             proofs=None, height: int = SLICE_TREE_HEIGHT, window_bytes: int = 0) -> None:
+    """te_encode_commit_batch_host: BlobEncoder::encode_with_proofs (sdk/src/codec/encoder.rs:220-260)
+    over a batch, host -> host: slices to `out` as encode_batch_host, plus per object n leaf hashes
+    (`leaf_hashes`, nobj*n*32 bytes), the root (`roots`, nobj*32) and, if `proofs` is given, the n
+    proofs of `height` hashes each (nobj*n*height*32).  Host buffers (pinned for PCIe rate)."""
+    arr = objs if _is_desc(objs) else encode_descs(objs)
+    cfg = slicer._cfg()
+    pp = C.c_void_p(_host_ptr(proofs)) if proofs is not None else None
+    r = lib.te_encode_commit_batch_host(slicer.coder.handle, C.byref(cfg), C.c_void_p(_host_ptr(data)), arr, len(arr),
+                                        C.c_void_p(_host_ptr(out)), height, C.c_void_p(_host_ptr(leaf_hashes)),
+                                        C.c_void_p(_host_ptr(roots)), pp, window_bytes)
     _check(r, "encode")
 
 

@@ -262,6 +262,7 @@ struct te_clay {
         hipStream_t s = nullptr;
         Arena arena;
         DevBuf in, out;
+        DevBuf commit;  // te_encode_commit_batch_host: the window's leaf hashes, roots, proofs
     } pipe[kPipe];
 };
 
@@ -291,6 +292,7 @@ static void release_device_state(te_clay *c) {
         sl.arena.release();
         sl.in.release();
         sl.out.release();
+        sl.commit.release();
         if (sl.s) (void)hipStreamDestroy(sl.s);
         sl.s = nullptr;
     }
@@ -1064,32 +1066,31 @@ int build_plan(const te_clay *c, int rotated, uint32_t lost, const uint32_t *ava
 
 }  // namespace
 
-// ------------------------------------------------------------------------------------------
-// C ABI: compute entry points
-// ------------------------------------------------------------------------------------------
-extern "C" {
+// Host -> host encode pipeline (te_encode_batch_host), optionally with the slice commitments of
+// BlobEncoder::encode_with_proofs (sdk/src/codec/encoder.rs:220-260): per object the n leaf hashes,
+// the root and n proofs, computed on the device from the window's slices before they leave HBM.
+struct CommitOut {
+    uint8_t *leaf, *root, *proof;  // host: nobj * n * 32, nobj * 32, nobj * n * height * 32 (or null)
+    uint32_t height;
+};
 
-int te_encode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, const te_object *objs,
-                           size_t nobj, uint8_t *d_out, void *stream) {
-    if (!c || !cfg || (!objs && nobj)) return TE_ERR_INVALID_ARG;
-    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
-    std::lock_guard<std::mutex> lk(c->mu);
-    DeviceGuard dg(c->device);
-    TE_HIP(dg.err);
-    return encode_enqueue(c, cfg, d_data, objs, nobj, d_out, (hipStream_t)stream, false);
-}
-
-int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data, const te_object *objs,
-                         size_t nobj, uint8_t *h_out, size_t window_bytes) {
+static int encode_host_impl(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data, const te_object *objs,
+                            size_t nobj, uint8_t *h_out, size_t window_bytes, const CommitOut *co) {
     if (!c || !cfg || (!objs && nobj) || (nobj && (!h_data || !h_out))) return TE_ERR_INVALID_ARG;
     if (device_count() <= 0) return TE_ERR_NO_DEVICE;
     if (window_bytes == 0) window_bytes = (size_t)1 << 30;
-    std::vector<uint64_t> out_bytes(nobj);
+    const uint32_t n = (uint32_t)c->h.n;
+    std::vector<uint64_t> out_bytes(nobj), slice_len(nobj);
     for (size_t i = 0; i < nobj; i++) {
         te_geometry g;
         te_slicer_geometry(c, objs[i].blob_len, &g);
-        out_bytes[i] = (uint64_t)c->h.n * g.slice_len;
+        slice_len[i] = g.slice_len;
+        out_bytes[i] = (uint64_t)n * g.slice_len;
+        if (co && g.slice_len % 4) return TE_ERR_INVALID_ARG;  // the leaf kernel reads dwords
     }
+    // per-object commitment bytes (device layout within a window: leaves, then roots, then proofs)
+    const uint64_t leaf_b = (uint64_t)n * TE_HASH_SIZE, proof_b = co && co->proof ? leaf_b * co->height : 0;
+
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
     TE_HIP(dg.err);
@@ -1138,6 +1139,37 @@ int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_
         rc = encode_enqueue(c, cfg, sl.in.as<uint8_t>(), local.data(), local.size(), sl.out.as<uint8_t>(), sl.s,
                             false, &sl.arena);
         if (rc) break;
+        if (co) {  // commitments of the window's objects, one launch per run of equal slice lengths
+            const uint64_t cnt = j - i;
+            const uint64_t root_at = cnt * leaf_b, proof_at = root_at + cnt * TE_HASH_SIZE;
+            if ((rc = hip_status(sl.commit.ensure(proof_at + cnt * proof_b)))) break;
+            uint8_t *dc = sl.commit.as<uint8_t>();
+            for (size_t o = i; o < j && rc == TE_OK;) {
+                size_t e = o + 1;
+                while (e < j && slice_len[e] == slice_len[o]) e++;
+                CommitArgs a{};
+                a.slices = sl.out.as<uint8_t>() + local[o - i].out_off;
+                a.obj_stride = out_bytes[o];
+                a.slice_len = slice_len[o];
+                a.n = n;
+                a.nobj = (uint32_t)(e - o);
+                a.height = co->height;
+                a.leaf = dc + (o - i) * leaf_b;
+                a.root = dc + root_at + (o - i) * TE_HASH_SIZE;
+                a.proof = co->proof ? dc + proof_at + (o - i) * proof_b : nullptr;
+                rc = hip_status(launch_commit(a, sl.s));
+                o = e;
+            }
+            if (rc) break;
+            const struct { uint8_t *h; uint64_t d, len; } back[3] = {
+                {co->leaf + i * leaf_b, 0, cnt * leaf_b},
+                {co->root + i * TE_HASH_SIZE, root_at, cnt * TE_HASH_SIZE},
+                {co->proof ? co->proof + i * proof_b : nullptr, proof_at, cnt * proof_b}};
+            for (const auto &bk : back)
+                if (bk.h && bk.len && (rc = hip_status(hipMemcpyAsync(bk.h, dc + bk.d, bk.len, hipMemcpyDeviceToHost, sl.s))))
+                    break;
+            if (rc) break;
+        }
         for (const Run &r : hout)
             if ((rc = hip_status(hipMemcpyAsync(h_out + r.host, sl.out.as<uint8_t>() + r.dev, r.len,
                                                 hipMemcpyDeviceToHost, sl.s))))
@@ -1152,6 +1184,37 @@ int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_
     return rc;
 }
 
+// ------------------------------------------------------------------------------------------
+// C ABI: compute entry points
+// ------------------------------------------------------------------------------------------
+extern "C" {
+
+int te_encode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, const te_object *objs,
+                           size_t nobj, uint8_t *d_out, void *stream) {
+    if (!c || !cfg || (!objs && nobj)) return TE_ERR_INVALID_ARG;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    TE_HIP(dg.err);
+    return encode_enqueue(c, cfg, d_data, objs, nobj, d_out, (hipStream_t)stream, false);
+}
+
+int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data, const te_object *objs,
+                         size_t nobj, uint8_t *h_out, size_t window_bytes) {
+    return encode_host_impl(c, cfg, h_data, objs, nobj, h_out, window_bytes, nullptr);
+}
+
+int te_encode_commit_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data, const te_object *objs,
+                                size_t nobj, uint8_t *h_out, uint32_t height, uint8_t *h_leaf_hashes,
+                                uint8_t *h_roots, uint8_t *h_proofs, size_t window_bytes) {
+    if (!c || !h_leaf_hashes || !h_roots || height == 0 || height > TE_MAX_MERKLE_TREE_HEIGHT)
+        return TE_ERR_INVALID_ARG;
+    const uint32_t n = (uint32_t)c->h.n;
+    if (n > TE_COMMIT_MAX_LEAVES) return TE_ERR_INVALID_ARG;
+    if (height < 64 && (uint64_t)n > (1ull << height)) return TE_ERR_MERKLE_TREE_FULL;
+    const CommitOut co{h_leaf_hashes, h_roots, h_proofs, height};
+    return encode_host_impl(c, cfg, h_data, objs, nobj, h_out, window_bytes, &co);
+}
 int te_encode_batch_host_multi(te_clay *const *coders, size_t ncoders, const te_slicer_cfg *cfg, const uint8_t *h_data,
                                const te_object *objs, size_t nobj, uint8_t *h_out, size_t window_bytes) {
     if (!coders || ncoders == 0 || !cfg || (!objs && nobj)) return TE_ERR_INVALID_ARG;

@@ -228,3 +228,43 @@ def test_odd_offsets_encode_decode(oracle, sizes):
     for i, L in enumerate(sizes):
         assert np.array_equal(dec[dec_off[i]:dec_off[i] + L], datas[i]), i
     assert not dec[:3].any() and not dec[c:].any()  # nothing written outside the objects
+
+
+@pytest.mark.parametrize("window", [0, 24 * MiB])
+def test_encode_commit_batch_host(oracle, window):
+    """te_encode_commit_batch_host = BlobEncoder::encode_with_proofs per object (encoder.rs:220-260)
+    over a host -> host pipeline: slices equal the oracle's, leaf hashes / roots / proofs equal the
+    merkle oracle's; mixed sizes (runs of equal slice length), an empty blob, several windows."""
+    import torch
+    from oracle import merkle_oracle as O
+    s = T.Slicer.clay_default()
+    sizes = [4 * MiB, 4 * MiB, 4 * MiB, 1_000_003, 0, 77, 3 * MiB + 5, 3 * MiB + 5]
+    geo = [s.geometry(L) for L in sizes]
+    in_off, out_off, a, b = [], [], 0, 0
+    for L, g in zip(sizes, geo):
+        in_off.append(a)
+        out_off.append(b)
+        a += L
+        b += N * g.slice_len
+    datas = [oracle.splitmix64_bytes(i + 71, L) for i, L in enumerate(sizes)]
+    h_in = torch.empty(max(1, a), dtype=torch.uint8).pin_memory()
+    for i, d in enumerate(datas):
+        h_in[in_off[i]:in_off[i] + sizes[i]] = torch.from_numpy(d)
+    h_out = torch.zeros(b, dtype=torch.uint8).pin_memory()
+    nobj, H = len(sizes), T.SLICE_TREE_HEIGHT
+    leaf = torch.zeros(nobj * N * 32, dtype=torch.uint8).pin_memory()
+    root = torch.zeros(nobj * 32, dtype=torch.uint8).pin_memory()
+    proof = torch.zeros(nobj * N * H * 32, dtype=torch.uint8).pin_memory()
+    objs = [(in_off[i], sizes[i], out_off[i], i) for i in range(nobj)]
+    batch.encode_commit_batch_host(s, h_in, objs, h_out, leaf, root, proof, window_bytes=window)
+    o = oracle.OracleClay(20, 7, 16)
+    got, lb, rb, pb = (t.numpy().tobytes() for t in (h_out, leaf, root, proof))
+    for i, L in enumerate(sizes):
+        sl_len = geo[i].slice_len
+        exp = oracle.slicer_encode(o, datas[i].tobytes(), chunk_index=i)
+        assert got[out_off[i]:out_off[i] + N * sl_len] == b"".join(exp), i
+        leaves, r, proofs = O.commit_slices(exp, H)
+        assert lb[i * N * 32:(i + 1) * N * 32] == b"".join(leaves), i
+        assert rb[i * 32:(i + 1) * 32] == r, i
+        gp = [[pb[((i * N + j) * H + l) * 32:((i * N + j) * H + l + 1) * 32] for l in range(H)] for j in range(N)]
+        assert gp == proofs, i

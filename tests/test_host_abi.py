@@ -190,3 +190,25 @@ def test_recover_needs_device():
     r = _lib.lib.te_recover_batch_device(c, C.byref(cfg), C.c_void_p(16), C.byref(obj), meta, 1, C.c_void_p(16), None)
     assert r == _lib.TE_ERR_NO_DEVICE
     _lib.lib.te_clay_free(c)
+
+
+def test_encode_commit_argument_checks():
+    """te_encode_commit_batch_host validates the tree before touching a device: height 0 or > 32
+    is an invalid argument, n = 20 leaves in a height-4 tree is TREE_FULL (tree.rs:344-350)."""
+    import ctypes as C
+    from tape_amd import _lib
+    c = C.c_void_p()
+    assert _lib.lib.te_clay_new(20, 7, 16, C.byref(c)) == 0
+    cfg = _lib.te_slicer_cfg()
+    obj = _lib.te_object(0, 1000, 0, 0)
+    buf = C.c_void_p(16)
+
+    def call(height):
+        return _lib.lib.te_encode_commit_batch_host(c, C.byref(cfg), buf, C.byref(obj), 1, buf, height, buf, buf,
+                                                    None, 0)
+    assert call(0) == _lib.TE_ERR_INVALID_ARG
+    assert call(33) == _lib.TE_ERR_INVALID_ARG
+    assert call(4) == _lib.TE_ERR_MERKLE_TREE_FULL
+    if _lib.device_count() == 0:
+        assert call(5) == _lib.TE_ERR_NO_DEVICE
+    _lib.lib.te_clay_free(c)
