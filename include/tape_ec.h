@@ -186,6 +186,21 @@ size_t te_extract_repair_data_size(const te_repair_plan *p, uint32_t helper_slic
 /* extract_repair_data  repair.rs:97-130 (helper-side gather; host only) */
 int te_extract_repair_data(const te_repair_plan *p, const uint8_t *slice, size_t slice_len,
                            uint32_t helper_slice, uint8_t *out, size_t cap, size_t *out_len);
+/* per_helper_reqs (network/node/src/features/spool/repair.rs:468-491) for one helper: the
+ * RepairRequest (network/protocol/src/api/types.rs:75-85) the repairing node sends helper slice
+ * `helper_slice` -- one StripeSubChunkRequest {stripe, sub_chunks} per stripe the helper serves,
+ * in plan order; stripe k at stripes[k], its beta sub-chunk indices at sub_chunks[k*beta].
+ * *count = the number of stripes (arrays NULL: count only). */
+int te_repair_plan_helper_request(const te_repair_plan *p, uint32_t helper_slice, uint32_t *stripes,
+                                  uint32_t *sub_chunks, size_t cap_stripes, size_t *count);
+/* The helper node's extract_repair_data (network/node/src/features/spool/repair.rs:496-553):
+ * serve a RepairRequest from the stored slice alone -- geometry from its metadata suffix and the
+ * coder's alpha; stripe i's nsub[i] sub-chunk indices are consecutive in sub_chunks; output is
+ * every requested sub-chunk in request order.  Layout errors return TE_ERR_INVALID_LAYOUT with
+ * the reference's message in te_last_error_detail().  Host only. */
+int te_serve_repair_request(te_clay *c, const uint8_t *slice, size_t slice_len, const uint32_t *stripes,
+                            const uint32_t *nsub, const uint32_t *sub_chunks, size_t nstripes, uint8_t *out,
+                            size_t cap, size_t *out_len);
 /* Slicer::repair  repair.rs:324-367: helper_data/helper_lens indexed by SLICE id (n entries,
  * NULL = not provided).  out = num_stripes*chunk_size + 48 bytes.  (GPU) */
 int te_slicer_repair(te_clay *c, const te_repair_plan *p, const uint8_t *const *helper_data,

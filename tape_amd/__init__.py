@@ -10,5 +10,5 @@ from .slicer import (  # noqa: F401
     ClayCoder, ClayParams, DecodeError, EncodeError, EncodingProfile, EncodingType, EngineError, HelperPlan,
     MappingStrategy, NoDeviceError, RepairError, RepairPlan, SliceMetadata, Slicer, StripeRepair,
     DEFAULT_STRIPE_SIZE, GROUP_SIZE, ROTATION_STEP, SLICE_TREE_HEIGHT, STRIPE_SIZES, extract_repair_data,
-    num_stripes, pick_stripe_size, shard_to_slice, slice_to_shard,
+    repair_request, serve_repair_request, num_stripes, pick_stripe_size, shard_to_slice, slice_to_shard,
 )

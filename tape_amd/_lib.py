@@ -137,6 +137,8 @@ def _load() -> C.CDLL:
         "te_extract_repair_data_size": (sz, [vp, u32]),
         "te_extract_repair_data": (i, [vp, u8p, sz, u32, u8p, sz, szp]),
         "te_slicer_repair": (i, [vp, vp, pp, szp, u8p, u8p, sz]),
+        "te_repair_plan_helper_request": (i, [vp, u32, u32p, u32p, sz, szp]),
+        "te_serve_repair_request": (i, [vp, u8p, sz, u32p, u32p, u32p, sz, u8p, sz, szp]),
         "te_encode_batch_device": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz, vp, vp]),
         "te_encode_batch_host": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz, vp, sz]),
         "te_encode_batch_host_multi": (i, [C.POINTER(vp), sz, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz,

@@ -1634,6 +1634,62 @@ int te_extract_repair_data(const te_repair_plan *p, const uint8_t *slice, size_t
     return TE_OK;
 }
 
+int te_repair_plan_helper_request(const te_repair_plan *p, uint32_t helper, uint32_t *stripes, uint32_t *sub_chunks,
+                                  size_t cap_stripes, size_t *count) {
+    if (!p || !count) return TE_ERR_INVALID_ARG;
+    size_t k = 0;
+    for (uint32_t st = 0; st < p->ns; st++)
+        for (uint32_t j = 0; j < p->d; j++) {
+            if (p->helper_slice[st * p->d + j] != helper) continue;
+            if (k < cap_stripes && stripes && sub_chunks) {
+                stripes[k] = st;
+                memcpy(sub_chunks + k * p->beta, &p->sub_chunks[(st * p->d + j) * p->beta], p->beta * sizeof(uint32_t));
+            }
+            k++;
+        }
+    *count = k;
+    return k <= cap_stripes || (!stripes && !sub_chunks) ? TE_OK : TE_ERR_BUFFER_TOO_SMALL;
+}
+
+int te_serve_repair_request(te_clay *c, const uint8_t *slice, size_t slice_len, const uint32_t *stripes,
+                            const uint32_t *nsub, const uint32_t *sub_chunks, size_t nstripes, uint8_t *out, size_t cap,
+                            size_t *out_len) {
+    if (!c || !slice || (nstripes && (!stripes || !nsub))) return TE_ERR_INVALID_ARG;
+    auto fail = [](const char *why) {
+        snprintf(g_last_error, sizeof(g_last_error), "%s", why);
+        return TE_ERR_INVALID_LAYOUT;
+    };
+    te_slice_metadata m;
+    if (slice_len < TE_META_SIZE) return fail("slice too short for metadata");
+    if (te_slice_metadata_from_slice(slice, slice_len, &m) != TE_OK) return fail("parse slice metadata failed");
+    if (m.blob_len && !m.stripe_size) return fail("parse slice metadata failed: zero stripe size");
+    const uint64_t ns = m.blob_len == 0 ? 1 : (m.blob_len + m.stripe_size - 1) / m.stripe_size;
+    const uint64_t total = slice_len - TE_META_SIZE;
+    if (total == 0 || total % ns) return fail("slice layout is inconsistent");
+    const uint64_t cs = total / ns, alpha = (uint64_t)c->h.alpha;
+    if (cs % alpha) return fail("chunk size is not divisible by alpha");
+    const uint64_t sc = cs / alpha;
+    uint64_t need = 0;
+    size_t at = 0;
+    for (size_t i = 0; i < nstripes; i++) {
+        const uint64_t c0 = (uint64_t)stripes[i] * cs;
+        if (c0 + cs > total + TE_META_SIZE) return fail("slice too short for requested stripe");
+        for (uint32_t b = 0; b < nsub[i]; b++, at++)
+            if (!sub_chunks || ((uint64_t)sub_chunks[at] + 1) * sc > cs) return fail("sub-chunk out of bounds");
+        need += (uint64_t)nsub[i] * sc;
+    }
+    if (out_len) *out_len = (size_t)need;
+    if (cap < need || (!out && need)) return TE_ERR_BUFFER_TOO_SMALL;
+    uint64_t w = 0;
+    at = 0;
+    for (size_t i = 0; i < nstripes; i++)
+        for (uint32_t b = 0; b < nsub[i]; b++, at++) {
+            memcpy(out + w, slice + (uint64_t)stripes[i] * cs + (uint64_t)sub_chunks[at] * sc, sc);
+            w += sc;
+        }
+    return TE_OK;
+}
+
 int te_slicer_repair(te_clay *c, const te_repair_plan *p, const uint8_t *const *helper_data, const size_t *helper_lens,
                      const uint8_t metadata[TE_META_SIZE], uint8_t *out, size_t cap) {
     if (!c || !p || !helper_data || !helper_lens || !metadata || !out) return TE_ERR_INVALID_ARG;

@@ -374,6 +374,7 @@ class RepairPlan:
         self.chunk_size = int(info.chunk_size)
         self.sub_chunk_size = int(info.sub_chunk_size)
         d, b = int(info.d), int(info.beta)
+        self.beta = b
         self.stripes: list[StripeRepair] = []
         for s in range(self.num_stripes):
             ls = C.c_uint32()
@@ -406,6 +407,39 @@ def extract_repair_data(slice_bytes: bytes, plan: RepairPlan, helper: int) -> by
     if r == _lib.TE_ERR_INVALID_LAYOUT:
         raise RepairError("InvalidLayout", "slice too short for chunk / sub-chunk out of bounds")
     _check(r, "repair")
+    return bytes(out)[:got.value]
+
+
+def repair_request(plan: RepairPlan, helper: int) -> list[tuple[int, list[int]]]:
+    """per_helper_reqs (network/node/src/features/spool/repair.rs:468-491) for one helper: the
+    RepairRequest.stripes (network/protocol/src/api/types.rs:75-85) as [(stripe, sub_chunks)]."""
+    cnt = C.c_size_t()
+    _check(lib.te_repair_plan_helper_request(plan.handle, helper, None, None, 0, C.byref(cnt)), "repair")
+    n = cnt.value
+    beta = plan.beta
+    st = (C.c_uint32 * max(1, n))()
+    sub = (C.c_uint32 * max(1, n * beta))()
+    _check(lib.te_repair_plan_helper_request(plan.handle, helper, st, sub, n, C.byref(cnt)), "repair")
+    return [(int(st[k]), [int(x) for x in sub[k * beta:(k + 1) * beta]]) for k in range(n)]
+
+
+def serve_repair_request(coder: ClayCoder, slice_bytes: bytes, stripes: list[tuple[int, list[int]]]) -> bytes:
+    """The helper node's extract_repair_data (network/node/src/features/spool/repair.rs:496-553):
+    the requested sub-chunks of a stored slice, geometry from the slice's own metadata suffix."""
+    ns = len(stripes)
+    st = (C.c_uint32 * max(1, ns))(*[s for s, _ in stripes])
+    nsub = (C.c_uint32 * max(1, ns))(*[len(z) for _, z in stripes])
+    flat = [z for _, zs in stripes for z in zs]
+    sub = (C.c_uint32 * max(1, len(flat)))(*flat)
+    got = C.c_size_t()
+    args = (coder.handle, _buf(slice_bytes), len(slice_bytes), st, nsub, sub, ns)
+    r = lib.te_serve_repair_request(*args, None, 0, C.byref(got))
+    if r == _lib.TE_ERR_INVALID_LAYOUT:
+        raise RepairError("InvalidLayout", _lib.lib.te_last_error_detail().decode())
+    if r not in (_lib.TE_OK, _lib.TE_ERR_BUFFER_TOO_SMALL):
+        _check(r, "repair")
+    out = (C.c_uint8 * max(1, got.value))()
+    _check(lib.te_serve_repair_request(*args, out, got.value, C.byref(got)), "repair")
     return bytes(out)[:got.value]
 
 

@@ -268,3 +268,18 @@ def test_encode_commit_batch_host(oracle, window):
         assert rb[i * 32:(i + 1) * 32] == r, i
         gp = [[pb[((i * N + j) * H + l) * 32:((i * N + j) * H + l + 1) * 32] for l in range(H)] for j in range(N)]
         assert gp == proofs, i
+
+
+def test_node_repair_over_the_wire(oracle):
+    """The node's repair_track flow (network/node/src/features/spool/repair.rs:271-350, test
+    clay_repair): plan, one RepairRequest per helper, each helper serves it from its stored slice,
+    Slicer::repair on the GPU rebuilds the lost slice."""
+    s = T.Slicer.clay_default()
+    data = oracle.splitmix64_bytes(0xC1A7, 3_000_001).tobytes()
+    sl = s.encode(data)
+    for lost in (2, 17):
+        avail = [i for i in range(N) if i != lost]
+        plan = s.repair_plan(lost, avail, sl[avail[0]])
+        served = {h: T.serve_repair_request(s.coder, sl[h], T.repair_request(plan, h)) for h in avail}
+        served = {h: v for h, v in served.items() if v}
+        assert s.repair(plan, served, sl[avail[0]][-48:]) == sl[lost], lost

@@ -212,3 +212,48 @@ def test_encode_commit_argument_checks():
     if _lib.device_count() == 0:
         assert call(5) == _lib.TE_ERR_NO_DEVICE
     _lib.lib.te_clay_free(c)
+
+
+def test_repair_request_round_trip(oracle):
+    """The node repair wire: per_helper_reqs (node repair.rs:468-491) inverts the
+    plan into one RepairRequest per helper (protocol types.rs:75-85); the helper serves it from its
+    stored slice alone (node repair.rs:496-553).  Served bytes equal the plan-side
+    extract_repair_data (slicer repair.rs:97-130) and the oracle's, for every helper."""
+    o = oracle.OracleClay(20, 7, 16)
+    s = T.Slicer.clay_default()
+    for L in (1, 300_000, 2_500_001):
+        data = oracle.splitmix64_bytes(L, L).tobytes()
+        sl = oracle.slicer_encode(o, data)
+        for lost in (0, 12):
+            avail = [i for i in range(N) if i != lost]
+            p = s.repair_plan(lost, avail, sl[avail[0]])
+            cs, stripes = oracle.repair_plan(o, lost, avail, L, T.pick_stripe_size(L), True)
+            served_from = set()
+            for h in avail:
+                req = T.repair_request(p, h)
+                exp_req = [(st, planes) for (st, _ls, helpers) in stripes for (slc, _sh, planes) in helpers if slc == h]
+                assert req == exp_req, (L, lost, h)
+                got = T.serve_repair_request(s.coder, sl[h], req)
+                assert got == T.extract_repair_data(sl[h], p, h) == oracle.extract_repair_data(sl[h], cs, o.alpha,
+                                                                                               stripes, h)
+                if req:
+                    served_from.add(h)
+            assert len(served_from) >= s.coder.d()
+
+
+def test_serve_repair_request_errors(oracle):
+    """extract_repair_data's error strings (node repair.rs:507-546) via te_last_error_detail."""
+    o = oracle.OracleClay(20, 7, 16)
+    s = T.Slicer.clay_default()
+    sl = oracle.slicer_encode(o, oracle.splitmix64_bytes(5, 2_500_000).tobytes())[3]
+    cases = [
+        (sl[:40], [(0, [0])], "slice too short for metadata"),
+        (sl[:1000] + sl[-48:], [(0, [0])], "slice layout is inconsistent"),
+        (sl, [(3, [0])], "slice too short for requested stripe"),
+        (sl, [(0, [100])], "sub-chunk out of bounds"),
+    ]
+    for blob, req, msg in cases:
+        with pytest.raises(T.RepairError) as e:
+            T.serve_repair_request(s.coder, blob, req)
+        assert msg in str(e.value), (msg, str(e.value))
+    assert T.serve_repair_request(s.coder, sl, []) == b""
