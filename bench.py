@@ -89,7 +89,7 @@ KERNELS = {
     "encode": ["tec::dma::enc_dma_kernel<false>"],
     "repair": ["tec::rfold::rep_fold_kernel<0, 6>", "tec::rfold::rep_fold_kernel<1, 6>"],
     "decode": ["tec::dstage::dec_stage_kernel<7, 6>"],
-    "commit": ["tec::leaf_kernel", "tec::tree_kernel"],
+    "commit": ["tec::commit::leaf_kernel", "tec::commit::tree_kernel"],
 }
 
 
