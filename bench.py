@@ -117,7 +117,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--objects", type=int, default=1024, help="objects per GPU per step")
     ap.add_argument("--object-bytes", type=int, default=4 * MiB)
-    ap.add_argument("--mode", choices=["encode", "repair", "decode", "commit", "recover"], default="encode")
+    ap.add_argument("--mode", choices=["encode", "repair", "decode", "commit", "recover", "outer"], default="encode")
+    ap.add_argument("--segments", type=int, default=16,
+                    help="--mode outer: snapshot segments per step (OuterCoder(17, 50), 4 MiB chunks)")
     ap.add_argument("--cpu-sample", type=int, default=96, help="objects in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = min(16, affinity cores): the GPU box grants 16 host cores per GPU (pool rules)")
@@ -139,6 +141,8 @@ def main():
     torch.cuda.set_device(dev)
     T.lib.te_set_device(dev.index)
 
+    if args.mode == "outer":
+        return outer_bench(args, torch, dist, world, rank, dev)
     L, nobj = args.object_bytes, args.objects
     slicer = T.Slicer.clay_default()
     g = slicer.geometry(L)
@@ -328,6 +332,63 @@ def main():
             "outputs_verified": verified,
         }
         print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def outer_bench(args, torch, dist, world, rank, dev):
+    """--mode outer: OuterCoder(17, 50).encode of snapshot segments on the GPU
+    (lib/snapshot/src/encode.rs:66-76 -> lib/slicer/src/outer.rs:70-118), 4 MiB chunks (the
+    codec's maximum): per segment 17 x 4 MiB of data in, 33 x 4 MiB of recovery chunks out."""
+    from tape_amd import outer
+    k, n, cb = 17, 50, 4 * MiB
+    m, segs = n - k, args.segments
+    first, _ = rank_objects(rank, segs)
+    d_in = torch.empty(segs * k * cb, dtype=torch.uint8, device=dev)
+    splitmix_fill(torch, d_in, first, segs, k * cb)
+    d_out = torch.empty(segs * m * cb, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        outer.encode_device(k, m, d_in, cb, segs, k * cb, d_out, m * cb, stream)
+
+    from tape_amd import batch
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    batch.kernel_time_ms()
+    batch.kernel_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(torch, dist, world, time.perf_counter() - t0, dev)
+    batch.kernel_timing(False)
+    kms, _ = batch.kernel_time_ms()
+    # the timed output: segment 0 decoded from its 17 parity-only chunks equals its data
+    seg0 = [d_out[j * cb:(j + 1) * cb].cpu().numpy().tobytes() for j in range(k)]
+    dec = outer.OuterCoder(k, n).decode([(k + j, seg0[j]) for j in range(k)])
+    verified = dec == d_in[:k * cb].cpu().numpy().tobytes()
+    alg = (k + m) * cb * segs
+    avg_s = kms / max(1, args.steps) / 1e3
+    if rank == 0:
+        print(json.dumps({
+            "metric": "device-resident OuterCoder(17, 50) encode GiB/s of snapshot data, 4 MiB chunks, 1 MI355X",
+            "value": round(segs * world * args.steps * k * cb / elapsed / 2**30, 3), "unit": "GiB/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u16 (GF(2^16))", "data": "synthetic SplitMix64, device-resident",
+            "config": {"workload": f"OuterCoder(17, 50).encode of {segs} segments of 17 x 4 MiB per GPU "
+                                   "(reed-solomon-simd Leopard GF(2^16) construction, parity unpinned)",
+                       "segments_per_gpu": segs, "chunk_bytes": cb, "parallelism": f"segments over {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": round(alg / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(alg / avg_s / 1e9 / PEAK_HBM_GBS, 4), "traffic": None,
+                         "alg_bytes_per_launch": alg, "avg_launch_ms": round(avg_s * 1e3, 4)},
+            "cpu_baseline": None, "outputs_verified": verified}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

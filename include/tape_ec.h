@@ -319,6 +319,32 @@ int te_commit_batch_device(const uint8_t *d_slices, uint64_t obj_stride, uint64_
                            size_t nobj, uint32_t height, uint8_t *d_leaf_hashes, uint8_t *d_roots,
                            uint8_t *d_proofs, void *hip_stream);
 
+/* ------------------------------------------------------------------------------------------
+ * OuterCoder (lib/slicer/src/outer.rs:19-197): single-level Reed-Solomon over
+ * GF(2^16) in the Leopard construction of reed-solomon-simd 3.1.0 (parity unpinned: the crate
+ * is not in the container).  n chunks, any k reconstruct; chunks 0..k-1 are the
+ * data (systematic), k..n-1 the crate's recovery shards.  Chunk bytes are 64-byte aligned
+ * (outer.rs:74-80), at most TE_OUTER_MAX_CHUNK_BYTES.
+ * ------------------------------------------------------------------------------------------ */
+#define TE_OUTER_MAX_CHUNK_BYTES (4u * 1024u * 1024u)  /* MAX_CHUNK_BYTES  outer.rs:12 */
+/* chunk size for `len` data bytes: ceil(len / k) rounded up to 64, 64 for empty data. */
+size_t te_outer_chunk_bytes(uint32_t k, size_t len);
+/* OuterCoder::encode (outer.rs:70-118): out = n chunks of *chunk_bytes (data zero-padded to
+ * k * chunk_bytes, then the n - k recovery chunks, computed on the GPU).  TE_ERR_TOO_MUCH_DATA
+ * past the chunk limit; TE_ERR_UNSUPPORTED for shard counts the codec does not support. */
+int te_outer_encode(uint32_t k, uint32_t n, const uint8_t *data, size_t len, uint8_t *out, size_t cap,
+                    size_t *chunk_bytes);
+/* OuterCoder::decode (outer.rs:126-197): chunks[i] for i < n (NULL = missing), all chunk_bytes
+ * long; out = the k data chunks (k * chunk_bytes, data padding included).  Missing data chunks
+ * are restored on the GPU from k received chunks.  TE_ERR_NOT_ENOUGH_SLICES below k chunks. */
+int te_outer_decode(uint32_t k, uint32_t n, const uint8_t *const *chunks, size_t chunk_bytes, uint8_t *out,
+                    size_t cap);
+/* Batched device form of the encode (DEVICE pointers): `segments` segments, segment g's k
+ * original shards at d_in + g*seg_in (shard j at + j*chunk_bytes), its m = n - k recovery shards
+ * to d_out + g*seg_out (shard j at + j*chunk_bytes).  Runs on hip_stream and waits for it. */
+int te_outer_encode_device(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t chunk_bytes, uint32_t segments,
+                           uint64_t seg_in, uint8_t *d_out, uint64_t seg_out, void *hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -157,6 +157,10 @@ def _load() -> C.CDLL:
         "te_merkle_proof_from_leaf_hashes": (i, [u8p, sz, sz, u32, u8p]),
         "te_merkle_verify_leaf_hash": (i, [u8p, u8p, u8p, sz, u64, u32]),
         "te_commit_batch_device": (i, [vp, u64, u64, u32, sz, u32, vp, vp, vp, vp]),
+        "te_outer_chunk_bytes": (sz, [u32, sz]),
+        "te_outer_encode": (i, [u32, u32, u8p, sz, u8p, sz, szp]),
+        "te_outer_decode": (i, [u32, u32, pp, sz, u8p, sz]),
+        "te_outer_encode_device": (i, [u32, u32, vp, u64, u32, u64, vp, u64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

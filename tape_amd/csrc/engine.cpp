@@ -20,6 +20,7 @@
 #include "sha256.hpp"
 #include <array>
 #include "clay_host.hpp"
+#include "rs16.hpp"
 #include "sha256.hpp"
 
 using namespace tec;
@@ -1885,6 +1886,142 @@ int te_commit_batch_device(const uint8_t *d_slices, uint64_t obj_stride, uint64_
     TE_HIP(launch_commit(a, s));
     kt.stop();
     return TE_OK;
+}
+
+
+// ------------------------------------------------------------------------------------------
+// OuterCoder: GF(2^16) Leopard RS (lib/slicer/src/outer.rs:19-197)
+// ------------------------------------------------------------------------------------------
+size_t te_outer_chunk_bytes(uint32_t k, size_t len) {  // outer.rs:74-80
+    if (k == 0) return 0;
+    if (len == 0) return 64;
+    const size_t raw = (len + k - 1) / k;
+    return (raw + 63) / 64 * 64;
+}
+
+int te_outer_encode_device(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t chunk_bytes, uint32_t segments,
+                           uint64_t seg_in, uint8_t *d_out, uint64_t seg_out, void *stream) {
+    if (k == 0 || m == 0 || !d_in || !d_out || chunk_bytes == 0 || chunk_bytes % 64 || chunk_bytes / 2 > 0xffffffffull)
+        return TE_ERR_INVALID_ARG;
+    if (rs16::use_high_rate(k, m) < 0) return TE_ERR_UNSUPPORTED;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    const rs16::Tables &T = rs16::tables();
+    const uint32_t c = rs16::chunk(k, m), span = rs16::skew_span(k, m), wl = rs16::work_len(k, m);
+    if ((size_t)span * 128 + (size_t)wl * 256 > 64 * 1024 || span > rs16::kModulus) return TE_ERR_UNSUPPORTED;
+    // nibble tables of every skew multiplier the transforms touch (zeros for the basis' zero)
+    std::vector<uint16_t> lut((size_t)span * 64, 0);
+    for (uint32_t sx = 0; sx < span; sx++) {
+        const uint16_t lm = T.skew[sx];
+        if (lm == rs16::kModulus) continue;
+        for (int q = 0; q < 4; q++)
+            for (uint32_t nb = 0; nb < 16; nb++) lut[(size_t)sx * 64 + q * 16 + nb] = T.mul((uint16_t)(nb << (4 * q)), lm);
+    }
+    hipStream_t s = (hipStream_t)stream;
+    uint16_t *d_lut = nullptr;
+    TE_HIP(hipMallocAsync((void **)&d_lut, lut.size() * sizeof(uint16_t), s));
+    int r = hip_status(hipMemcpyAsync(d_lut, lut.data(), lut.size() * sizeof(uint16_t), hipMemcpyHostToDevice, s));
+    if (r == TE_OK) {
+        Rs16EncArgs a{};
+        a.in = d_in;
+        a.out = d_out;
+        a.in_stride = a.out_stride = chunk_bytes;
+        a.seg_in = seg_in;
+        a.seg_out = seg_out;
+        a.lut = d_lut;
+        a.k = k; a.m = m; a.c = c; a.high = (uint32_t)rs16::use_high_rate(k, m);
+        a.work_len = wl; a.span = span; a.elems = (uint32_t)(chunk_bytes / 2);
+        KTimer kt(s);
+        r = hip_status(launch_rs16_encode(a, segments, s));
+        kt.stop();
+    }
+    const int r2 = hip_status(hipFreeAsync(d_lut, s));
+    if (r == TE_OK) r = hip_status(hipStreamSynchronize(s));  // the host table must outlive the copy
+    return r ? r : r2;
+}
+
+int te_outer_encode(uint32_t k, uint32_t n, const uint8_t *data, size_t len, uint8_t *out, size_t cap,
+                    size_t *chunk_bytes_out) {
+    if (k == 0 || k > n || (!data && len)) return TE_ERR_INVALID_ARG;
+    const size_t cb = te_outer_chunk_bytes(k, len);
+    if (chunk_bytes_out) *chunk_bytes_out = cb;
+    if (cb > TE_OUTER_MAX_CHUNK_BYTES) return TE_ERR_TOO_MUCH_DATA;  // outer.rs:82-84
+    if (!out || cap < (size_t)n * cb) return TE_ERR_BUFFER_TOO_SMALL;
+    if (len) memcpy(out, data, len);
+    memset(out + len, 0, (size_t)k * cb - len);
+    const uint32_t m = n - k;
+    if (m == 0) return TE_OK;
+    if (rs16::use_high_rate(k, m) < 0) return TE_ERR_UNSUPPORTED;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    uint8_t *d = nullptr;
+    TE_HIP(hipMalloc((void **)&d, (size_t)n * cb));
+    int r = hip_status(hipMemcpy(d, out, (size_t)k * cb, hipMemcpyHostToDevice));
+    if (r == TE_OK) r = te_outer_encode_device(k, m, d, cb, 1, 0, d + (size_t)k * cb, 0, nullptr);
+    if (r == TE_OK) r = hip_status(hipMemcpy(out + (size_t)k * cb, d + (size_t)k * cb, (size_t)m * cb, hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    return r;
+}
+
+int te_outer_decode(uint32_t k, uint32_t n, const uint8_t *const *chunks, size_t chunk_bytes, uint8_t *out, size_t cap) {
+    if (k == 0 || k > n || !chunks || !out) return TE_ERR_INVALID_ARG;
+    std::vector<uint32_t> have;
+    for (uint32_t i = 0; i < n; i++)
+        if (chunks[i]) have.push_back(i);
+    if (have.size() < k) return TE_ERR_NOT_ENOUGH_SLICES;   // outer.rs:127-129
+    if (cap < (size_t)k * chunk_bytes) return TE_ERR_BUFFER_TOO_SMALL;
+    const uint32_t m = n - k;
+    std::vector<uint32_t> miss;
+    for (uint32_t i = 0; i < k; i++) {
+        if (chunks[i]) memcpy(out + (size_t)i * chunk_bytes, chunks[i], chunk_bytes);
+        else miss.push_back(i);
+    }
+    if (miss.empty()) return TE_OK;
+    if (m == 0) return TE_ERR_INVALID_LAYOUT;                 // outer.rs:143-152
+    if (chunk_bytes == 0 || chunk_bytes % 64) return TE_ERR_INVALID_LAYOUT;  // the decoder's shard-size check
+    if (rs16::use_high_rate(k, m) < 0 || k > kRs16MaxK) return TE_ERR_UNSUPPORTED;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    std::vector<uint32_t> recv(have.begin(), have.begin() + k);  // any k shards determine the originals
+    std::vector<uint16_t> D;
+    if (!rs16::decode_matrix(k, m, recv, D)) return TE_ERR_INVALID_LAYOUT;
+    const rs16::Tables &T = rs16::tables();
+    const uint32_t nm = (uint32_t)miss.size();
+    std::vector<uint16_t> lut((size_t)nm * k * 64, 0);
+    for (uint32_t i = 0; i < nm; i++)
+        for (uint32_t r = 0; r < k; r++) {
+            const uint16_t coef = D[(size_t)miss[i] * k + r];
+            if (!coef) continue;
+            for (int q = 0; q < 4; q++)
+                for (uint32_t nb = 0; nb < 16; nb++)
+                    lut[((size_t)i * k + r) * 64 + q * 16 + nb] = T.gmul((uint16_t)(nb << (4 * q)), coef);
+        }
+    // device image: received shards, restored shards, pointer arrays, tables
+    const size_t sh = (size_t)k * chunk_bytes, rs = (size_t)nm * chunk_bytes;
+    const size_t ptr_at = sh + rs, lut_at = ptr_at + (size_t)(k + nm) * sizeof(void *);
+    uint8_t *d = nullptr;
+    TE_HIP(hipMalloc((void **)&d, lut_at + lut.size() * sizeof(uint16_t)));
+    std::vector<const uint8_t *> ptrs;
+    int r = TE_OK;
+    for (uint32_t j = 0; j < k && r == TE_OK; j++) {
+        ptrs.push_back(d + (size_t)j * chunk_bytes);
+        r = hip_status(hipMemcpy(d + (size_t)j * chunk_bytes, chunks[recv[j]], chunk_bytes, hipMemcpyHostToDevice));
+    }
+    for (uint32_t i = 0; i < nm; i++) ptrs.push_back(d + sh + (size_t)i * chunk_bytes);
+    if (r == TE_OK) r = hip_status(hipMemcpy(d + ptr_at, ptrs.data(), ptrs.size() * sizeof(void *), hipMemcpyHostToDevice));
+    if (r == TE_OK) r = hip_status(hipMemcpy(d + lut_at, lut.data(), lut.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    if (r == TE_OK) {
+        Rs16DecArgs a{};
+        a.recv = reinterpret_cast<const uint8_t *const *>(d + ptr_at);
+        a.out = reinterpret_cast<uint8_t *const *>(d + ptr_at + (size_t)k * sizeof(void *));
+        a.lut = reinterpret_cast<const uint16_t *>(d + lut_at);
+        a.k = k; a.nmiss = nm; a.elems = (uint32_t)(chunk_bytes / 2);
+        KTimer kt(nullptr);
+        r = hip_status(launch_rs16_decode(a, nullptr));
+        kt.stop();
+    }
+    for (uint32_t i = 0; i < nm && r == TE_OK; i++)
+        r = hip_status(hipMemcpy(out + (size_t)miss[i] * chunk_bytes, d + sh + (size_t)i * chunk_bytes, chunk_bytes,
+                                 hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    return r;
 }
 
 }  // extern "C"

@@ -212,6 +212,24 @@ struct CopyJob {
 };
 hipError_t launch_gather(const CopyJob *jobs, uint32_t njobs, hipStream_t s);
 hipError_t launch_gpe(const GpeArgs &a, uint32_t max_erased, hipStream_t s);
+
+// ---- GF(2^16) Leopard RS (rs16.hip) ----
+constexpr uint32_t kRs16MaxK = 64;  // decode: received shards per matrix row
+struct Rs16EncArgs {
+    const uint8_t *in;          // original shard j at in + seg * seg_in + j * in_stride
+    uint8_t *out;               // recovery shard j at out + seg * seg_out + j * out_stride
+    uint64_t in_stride, out_stride, seg_in, seg_out;
+    const uint16_t *lut;        // span x 64 nibble-table entries: multiplier = skew[s]
+    uint32_t k, m, c, high, work_len, span, elems;  // elems: field elements per shard (bytes / 2)
+};
+struct Rs16DecArgs {
+    const uint8_t *const *recv; // k received shards (device pointer array)
+    uint8_t *const *out;        // nmiss restored originals
+    const uint16_t *lut;        // nmiss x k nibble tables (decoding-matrix coefficients)
+    uint32_t k, nmiss, elems;
+};
+hipError_t launch_rs16_encode(const Rs16EncArgs &a, uint32_t segments, hipStream_t s);
+hipError_t launch_rs16_decode(const Rs16DecArgs &a, hipStream_t s);
 hipError_t launch_repair(const RepArgs &a, uint32_t max_erased, hipStream_t s);
 hipError_t launch_repair_stage(RepArgs a, hipStream_t s);
 // repair_fold.hip: Clay(20,7,16) with every other node available (the decoding matrix folded per

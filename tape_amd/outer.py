@@ -1,0 +1,68 @@
+"""OuterCoder (lib/slicer/src/outer.rs:19-197): single-level Reed-Solomon over GF(2^16)
+distributing data over n chunks such that any k reconstruct it -- the snapshot coder
+(lib/snapshot/src/encode.rs:66-76).  The codec is the Leopard construction of reed-solomon-simd
+3.1.0, run on the GPU by libtapeec (te_outer_*); parity unpinned against the absent crate."""
+from __future__ import annotations
+
+import ctypes as C
+
+from . import _lib
+from ._lib import lib
+from .slicer import DecodeError, EncodeError, _buf, _check
+
+MAX_CHUNK_BYTES = 4 * 1024 * 1024  # outer.rs:12
+
+
+class OuterCoder:
+    def __init__(self, k: int, n: int):
+        assert k > 0, "k must be > 0"      # outer.rs:30
+        assert k <= n, "k must be <= n"    # outer.rs:31
+        self._k, self._n = k, n
+
+    def k(self) -> int:
+        return self._k
+
+    def n(self) -> int:
+        return self._n
+
+    def m(self) -> int:
+        return self._n - self._k
+
+    def encode(self, data: bytes) -> list[bytes]:
+        """OuterCoder::encode (outer.rs:70-118): n chunks, the first k the zero-padded data."""
+        cb = int(lib.te_outer_chunk_bytes(self._k, len(data)))
+        out = (C.c_uint8 * (self._n * cb))()
+        got = C.c_size_t()
+        r = lib.te_outer_encode(self._k, self._n, _buf(data), len(data), out, len(out), C.byref(got))
+        _check(r, "encode")
+        raw = bytes(out)
+        return [raw[i * cb:(i + 1) * cb] for i in range(self._n)]
+
+    def decode(self, chunks: list[tuple[int, bytes]]) -> bytes:
+        """OuterCoder::decode (outer.rs:126-197): the k data chunks (with their padding)."""
+        if len(chunks) < self._k:
+            raise DecodeError("NotEnoughSlices")
+        cb = len(chunks[0][1])
+        if any(len(d) != cb for _, d in chunks) or any(i >= self._n or i < 0 for i, _ in chunks):
+            raise DecodeError("InvalidLayout")
+        ptrs = (C.c_void_p * self._n)()
+        keep = {}
+        for i, d in chunks:
+            keep[i] = C.create_string_buffer(bytes(d), cb)
+            ptrs[i] = C.cast(keep[i], C.c_void_p)
+        out = (C.c_uint8 * max(1, self._k * cb))()
+        r = lib.te_outer_decode(self._k, self._n, ptrs, cb, out, len(out))
+        _check(r, "decode")
+        return bytes(out)[:self._k * cb]
+
+
+def encode_device(k: int, m: int, d_in, chunk_bytes: int, segments: int, seg_in: int, d_out, seg_out: int,
+                  stream=None) -> None:
+    """te_outer_encode_device: `segments` OuterCoder encodes on device buffers (torch tensors)."""
+    sp = stream.cuda_stream if stream is not None else None
+    r = lib.te_outer_encode_device(k, m, C.c_void_p(d_in.data_ptr()), chunk_bytes, segments, seg_in,
+                                   C.c_void_p(d_out.data_ptr()), seg_out, C.c_void_p(sp) if sp else None)
+    _check(r, "encode")
+
+
+__all__ = ["OuterCoder", "encode_device", "MAX_CHUNK_BYTES", "EncodeError", "DecodeError", "_lib"]

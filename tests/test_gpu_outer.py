@@ -1,0 +1,86 @@
+"""GPU parity of the OuterCoder (lib/slicer/src/outer.rs:19-197) against the GF(2^16)
+Leopard RS oracle (oracle/rs16_oracle.c; parity unpinned vs reed-solomon-simd 3.1.0, which is not
+in the container): encoded chunks byte for byte, decodes against the original data, and the
+reference's own OuterCoder tests (outer.rs:206-391) on the GPU path."""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import rs16
+from tape_amd.outer import OuterCoder
+import tape_amd as T
+
+pytestmark = pytest.mark.gpu
+SPOOL_GROUP_COUNT, TEST_K = 50, 17
+
+
+def make_data(n):  # outer.rs:206-208
+    return bytes(i % 251 for i in range(n))
+
+
+@pytest.mark.parametrize("k,n", [(17, 50), (7, 50), (4, 6), (10, 14), (32, 64), (40, 49), (3, 8), (1, 2)])
+@pytest.mark.parametrize("size", [1, 1000, 100_003])
+def test_encode_matches_oracle(k, n, size):
+    data = np.random.default_rng(k * 1000 + n + size).bytes(size)
+    got = OuterCoder(k, n).encode(data)
+    exp = rs16.OracleOuter(k, n).encode(data)
+    assert len(got) == n and got == exp
+
+
+def test_encode_max_chunk_matches_oracle():
+    k, n = TEST_K, SPOOL_GROUP_COUNT
+    data = np.random.default_rng(7).bytes(k * (4 * 1024 * 1024) - 100)  # chunk = MAX_CHUNK_BYTES
+    got = OuterCoder(k, n).encode(data)
+    assert len(got[0]) == 4 * 1024 * 1024
+    exp = rs16.OracleOuter(k, n).encode(data)
+    assert got == exp
+    with pytest.raises(T.EncodeError):
+        OuterCoder(k, n).encode(bytes(k * 4 * 1024 * 1024 + 1))  # outer.rs:82-84 TooMuchData
+
+
+@pytest.mark.parametrize("k,n", [(17, 50), (7, 50), (10, 14), (32, 64)])
+def test_decode_patterns(k, n):
+    rnd = random.Random(k + n)
+    c = OuterCoder(k, n)
+    data = make_data(123_457)
+    ch = list(enumerate(c.encode(data)))
+    sets = [ch[:k], ch[n - k:], [x for x in ch if x[0] % 3 == 0][:k]] + \
+           [[ch[i] for i in sorted(rnd.sample(range(n), k))] for _ in range(6)]
+    for avail in sets:
+        if len(avail) < k:
+            continue
+        assert c.decode(avail)[:len(data)] == data, [i for i, _ in avail]
+
+
+def test_reference_outer_tests_on_gpu():  # outer.rs:210-390
+    c = OuterCoder(TEST_K, SPOOL_GROUP_COUNT)
+    ch = list(enumerate(c.encode(make_data(100_000))))
+    assert len(ch) == SPOOL_GROUP_COUNT and len({len(x) for _, x in ch}) == 1
+    with pytest.raises(T.DecodeError):
+        c.decode(ch[:TEST_K - 1])
+    e = list(enumerate(c.encode(b"")))
+    assert len(e[0][1]) == 64 and not any(c.decode(e[TEST_K:2 * TEST_K]))
+    for sz in (1, 13, TEST_K, 1000, 50_000, 200_000):
+        d = make_data(sz)
+        ch = list(enumerate(c.encode(d)))
+        assert c.decode(ch[:TEST_K])[:sz] == d and c.decode(ch[-TEST_K:])[:sz] == d
+    one = OuterCoder(1, 1)
+    d = make_data(10_000)
+    assert one.decode(list(enumerate(one.encode(d))))[:len(d)] == d
+
+
+def test_encode_device_segments():
+    import torch
+    from tape_amd import outer
+    k, m, cb, segs = TEST_K, SPOOL_GROUP_COUNT - TEST_K, 64 * 1024, 5
+    host = np.random.default_rng(3).integers(0, 256, segs * k * cb, dtype=np.uint8)
+    d_in = torch.from_numpy(host).cuda()
+    d_out = torch.zeros(segs * m * cb, dtype=torch.uint8, device="cuda")
+    outer.encode_device(k, m, d_in, cb, segs, k * cb, d_out, m * cb)
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy()
+    for g in (0, segs - 1):
+        shards = [host[(g * k + j) * cb:(g * k + j + 1) * cb].tobytes() for j in range(k)]
+        exp = b"".join(rs16.encode(k, m, shards))
+        assert got[g * m * cb:(g + 1) * m * cb].tobytes() == exp, g
