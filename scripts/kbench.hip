@@ -54,6 +54,7 @@ int main(int argc, char **argv) {
     for (int o = 0; o < nobj; o++)
         for (size_t s = 0; s < ns; s++) {
             EncJob j{};
+            j.store_mask = ~0u;
             j.src = din + (size_t)o * L + s * S;
             j.src_len = std::min<size_t>(S, L - s * S);
             j.dst = dout + (size_t)o * 20 * slen + s * cs;

@@ -224,6 +224,7 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
     const uint32_t dst_range = a.n * slen - J.dst_skew;  // < 2^31, host-checked
     const u32x4 rs_dst = rsrc(J.dst, dst_range);
     const __amdgpu_buffer_rsrc_t rb_dst = __builtin_amdgcn_make_buffer_rsrc(J.dst, 0, (int)dst_range, 0x00020000);
+    const uint32_t store_mask = J.store_mask;  // chunks to write (internal nodes)
     uint32_t sl_lane = lane + J.rot;
     sl_lane = (sl_lane >= 20u ? sl_lane - 20u : sl_lane) * slen;
     auto slice_off = [&](uint32_t node) -> uint32_t { return __builtin_amdgcn_readlane(sl_lane, node); };
@@ -396,6 +397,7 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
                     d1[q] = *reinterpret_cast<const u32x4 *>(row + lo1);
                     const uint32_t node = (it >> 8) & 0xffu, tz0 = (it >> 16) & 0xffu, ts = it >> 24;
                     dst[q] = slice_off(node) + ((tz0 == 0xffu ? z0 : tz0) * kQ + (ts == 0xffu ? s : ts)) * sc;
+                    if (!((store_mask >> node) & 1u)) dst[q] = kDrop;  // a chunk the caller does not keep
                 }
             }
             // B1: the next plane's DMA has landed (this wave's pieces are older than its last
@@ -423,7 +425,9 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
         const u32x4 e0 = *reinterpret_cast<const u32x4 *>(row + lo0);
         const u32x4 e1 = *reinterpret_cast<const u32x4 *>(row + lo1);
         const uint32_t node = (it >> 8) & 0xffu, tz0 = (it >> 16) & 0xffu, ts = it >> 24;
-        const uint32_t d = slice_off(node) + ((tz0 == 0xffu ? kQ - 1u : tz0) * kQ + (ts == 0xffu ? kQ - 1u : ts)) * sc;
+        const uint32_t d = ((store_mask >> node) & 1u)
+                               ? slice_off(node) + ((tz0 == 0xffu ? kQ - 1u : tz0) * kQ + (ts == 0xffu ? kQ - 1u : ts)) * sc
+                               : kDrop;
         if (!(TEC_DMA_ABLATE & 1)) {
             __builtin_amdgcn_raw_buffer_store_b128(e0, rb_dst, (int)vo0, (int)d, TEC_DMA_ST_AUX);
             __builtin_amdgcn_raw_buffer_store_b128(e1, rb_dst, (int)vo1, (int)d, TEC_DMA_ST_AUX);

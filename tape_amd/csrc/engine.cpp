@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <map>
+#include <unordered_map>
 #include <mutex>
 #include <vector>
 #include <algorithm>
@@ -259,6 +260,16 @@ struct te_clay {
     // te_encode_batch_host pipeline: kPipe slots, each with its own stream, descriptor arena
     // and device window buffers, so window w+1's H2D overlaps window w's kernel and D2H.
     static constexpr int kPipe = 3;
+    // Compiled decode patterns (layered pattern + staged plane program), by padded erasure mask:
+    // building them is host work per distinct pattern (matrix inversion, program, colouring).
+    struct DecCache {
+        GpePattern P;
+        std::vector<uint16_t> planes;  // P's plane list (P.planes_off is set per call)
+        bool staged = false;           // a plane program exists for the staged kernel
+        DecProgHdr H{};
+        std::vector<DecStepP> steps;   // packed program + 2 blank steps
+    };
+    std::unordered_map<uint64_t, DecCache> dec_cache;
     struct Slot {
         hipStream_t s = nullptr;
         Arena arena;
@@ -519,9 +530,12 @@ int ensure_stream(te_clay *c) {
 
 // Enqueue the encode of a batch.  raw = ClayCoder::encode semantics (no slicing/rotation/meta,
 // slices are the n chunks of one padded input).
-// keep(obj, stripe): which stripes to encode (all when empty); with a selector no metadata
-// suffix is written (te_recover_batch_device writes its own).
-using StripeSel = std::function<bool(size_t, size_t)>;
+// keep(obj, stripe): which stripes to encode and which of their chunks to write -- a mask of
+// internal nodes, 0 = skip the stripe (all stripes, all chunks when empty).  With a selector no
+// metadata suffix is written (te_recover_batch_device writes its own).  The mask is a store
+// filter of the LDS-DMA kernel (it must include the column-0 parity nodes, which that kernel
+// reads back); the other kernels write every chunk.
+using StripeSel = std::function<uint32_t(size_t, size_t)>;
 
 int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, const te_object *objs,
                    size_t nobj, uint8_t *d_out, hipStream_t s, bool raw, Arena *arena = nullptr,
@@ -548,8 +562,10 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
         }
         if (cs % (size_t)h.alpha || slice_len > 0xffffffffull || cs > 0xffffffffull) return TE_ERR_TOO_MUCH_DATA;
         for (size_t st = 0; st < ns; st++) {
-            if (keep && !keep(i, st)) continue;
+            const uint32_t store = keep ? keep(i, st) : ~0u;
+            if (!store) continue;
             EncJob j{};
+            j.store_mask = store;
             const uint64_t start = (uint64_t)st * S;
             j.src = d_data + o.data_off + start;
             j.src_len = o.blob_len == 0 ? 0 : std::min<uint64_t>(S, o.blob_len - start);
@@ -725,13 +741,52 @@ int decode_validate(const te_clay *c, const uint8_t *meta48, uint64_t slice_len,
     return TE_OK;
 }
 
+// The compiled form of one padded erasure pattern, built once per handle (caller holds c->mu).
+const te_clay::DecCache *dec_pattern(te_clay *c, uint64_t emask) {
+    auto f = c->dec_cache.find(emask);
+    if (f != c->dec_cache.end()) return &f->second;
+    const ClayHost &h = c->h;
+    const int n = h.n;
+    te_clay::DecCache d;
+    if (!h.gpe_pattern(emask, d.P, d.planes)) return nullptr;
+    d.P.planes_off = 0;
+    // staged kernel (decode_stage.hip): compiled per k with every other node erased (padded
+    // patterns); of the two row orientations, two workgroups per CU first (2 x 53 x 1536 B <=
+    // 160 KB), then fewer scratch rows
+    if (decode_stage_k(h.k) && d.P.nknown == (uint32_t)h.k && d.P.nerased == (uint32_t)(n - h.k)) {
+        DecProgHdr best{};
+        std::vector<DecStep> best_steps;
+        bool found = false;
+        auto cost = [](const DecProgHdr &x) {
+            return (decode_stage_rows(x.nslots, x.max_out) > 53 ? 1u << 20 : 0u) + x.nscratch;
+        };
+        for (int orient = 0; orient < 2; orient++) {
+            DecProgHdr H;
+            std::vector<DecStep> st;
+            if (!h.dec_prog(d.P, orient, H, st) || !decode_stage_fits(H.nslots, H.max_out)) continue;
+            if (!found || cost(H) < cost(best)) { best = H; best_steps.swap(st); found = true; }
+        }
+        bool ok = found;
+        for (const DecStep &S : best_steps) {
+            d.steps.emplace_back();
+            ok = ok && ClayHost::dec_pack(S, d.steps.back());
+        }
+        d.steps.resize(d.steps.size() + 2);  // blank steps: the kernel reads two steps ahead
+        d.staged = ok;
+        d.H = best;
+    }
+    return &c->dec_cache.emplace(emask, std::move(d)).first->second;
+}
+
 int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices, const DecItem *items,
                    size_t nitems, uint8_t *d_out, hipStream_t s, bool raw) {
     const ClayHost &h = c->h;
     const int n = h.n;
     const int rotated = (cfg && !raw) ? cfg->rotated : 0;
+    if (c->dec_cache.size() > 8192) c->dec_cache.clear();  // bounded (77,520 masks exist for k = 7)
     std::map<uint64_t, uint32_t> pat_index;  // erased mask -> pattern id
     std::vector<GpePattern> pats;
+    std::vector<const te_clay::DecCache *> cached;
     std::vector<uint16_t> pool;
     std::map<uint64_t, std::vector<GpeJob>> groups;  // by chunk size
     std::map<uint64_t, uint64_t> group_in_stride;
@@ -748,12 +803,15 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
             auto f = pat_index.find(emask);
             uint32_t pid;
             if (f == pat_index.end()) {
-                GpePattern P;
-                if (!h.gpe_pattern(emask, P, pool)) return TE_ERR_BAD_ENCODING;
+                const te_clay::DecCache *dc = dec_pattern(c, emask);
+                if (!dc) return TE_ERR_BAD_ENCODING;
                 pid = (uint32_t)pats.size();
-                pats.push_back(P);
+                pats.push_back(dc->P);
+                pats.back().planes_off = (uint32_t)pool.size();
+                pool.insert(pool.end(), dc->planes.begin(), dc->planes.end());
+                cached.push_back(dc);
                 pat_index[emask] = pid;
-                max_er = std::max(max_er, P.nerased);
+                max_er = std::max(max_er, dc->P.nerased);
             } else {
                 pid = f->second;
             }
@@ -778,36 +836,14 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     uint32_t lds_rows = 0, nscr_max = 0;
     bool staged = true;
     for (size_t i = 0; i < pats.size() && staged; i++) {
-        DecProgHdr best{};
-        std::vector<DecStep> best_steps;
-        bool found = false;
-        // the kernel is compiled per k, with every other node erased (padded patterns)
-        if (!decode_stage_k(h.k) || pats[i].nknown != (uint32_t)h.k || pats[i].nerased != (uint32_t)(n - h.k)) {
-            staged = false;
-            break;
-        }
-        for (int orient = 0; orient < 2; orient++) {
-            DecProgHdr H;
-            std::vector<DecStep> st;
-            if (!h.dec_prog(pats[i], orient, H, st) || !decode_stage_fits(H.nslots, H.max_out)) continue;
-            // rows for two workgroups per CU at 6 waves (2 x 53 x 1536 B <= 160 KB) first, then
-            // fewer scratch rows
-            auto cost = [](const DecProgHdr &x) {
-                return (decode_stage_rows(x.nslots, x.max_out) > 53 ? 1u << 20 : 0u) + x.nscratch;
-            };
-            if (!found || cost(H) < cost(best)) { best = H; best_steps.swap(st); found = true; }
-        }
-        staged = found;
-        if (!found) break;
-        dhdrs[i] = best;
+        const te_clay::DecCache &dc = *cached[i];
+        staged = dc.staged;
+        if (!staged) break;
+        dhdrs[i] = dc.H;
         dstep_off[i] = (uint32_t)dsteps.size();
-        for (const DecStep &S : best_steps) {
-            dsteps.emplace_back();
-            staged = staged && ClayHost::dec_pack(S, dsteps.back());
-        }
-        dsteps.resize(dsteps.size() + 2);  // blank steps: the kernel reads two steps ahead
-        lds_rows = std::max(lds_rows, decode_stage_rows(best.nslots, best.max_out));
-        nscr_max = std::max(nscr_max, best.nscratch);
+        dsteps.insert(dsteps.end(), dc.steps.begin(), dc.steps.end());
+        lds_rows = std::max(lds_rows, decode_stage_rows(dc.H.nslots, dc.H.max_out));
+        nscr_max = std::max(nscr_max, dc.H.nscratch);
     }
     lds_rows = std::max(lds_rows, 1u);
     Arena &A = c->dec;
@@ -1376,9 +1412,16 @@ int te_recover_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t 
         bool any_parity = false;
         for (size_t i = w.b; i < w.e && !any_parity; i++)
             for (uint64_t st = 0; st < nstripes[i]; st++) any_parity = any_parity || is_parity(i, st);
+        // parity-lost stripes are re-encoded writing only the lost shard's chunk (plus the
+        // column-0 parity chunks the LDS-DMA kernel reads back internally)
+        const uint32_t col0_parity = ((1u << h.q) - 1u) & ~((1u << h.k) - 1u);
         if (any_parity &&
             (r = encode_enqueue(c, cfg, blob, wenc.data(), wenc.size(), slices, s, false, nullptr,
-                                [&](size_t o, size_t st) { return is_parity(w.b + o, st); })))
+                                [&](size_t o, size_t st) -> uint32_t {
+                                    if (!is_parity(w.b + o, st)) return 0u;
+                                    return col0_parity | (1u << te_slice_to_shard(rotated, n, (uint32_t)st,
+                                                                                  objs[w.b + o].lost));
+                                })))
             break;
         // assemble the lost slices: per stripe the lost shard's chunk, then the suffix
         jobs.clear();

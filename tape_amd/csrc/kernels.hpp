@@ -13,7 +13,8 @@ struct EncJob {
     uint64_t src_len;     // valid bytes of the stripe (rest is zero padding)
     uint32_t rot;         // rotation offset (stripe*7) % n, 0 for identity mapping
     uint32_t dst_skew;    // stripe*chunk_size: dst - (object's slice-0 base)
-    uint64_t pad_;
+    uint32_t store_mask;  // internal nodes whose chunk is written (encode_dma.hip; others write all)
+    uint32_t pad_;
 };
 
 struct EncArgs {
