@@ -284,9 +284,9 @@ def main():
         copy_commit = copy_inclusive_commit(args, torch, dist, world, slicer, batch, d_in, d_out, per, L, dev)
 
     cpu = None
-    if rank == 0 and args.cpu_sample > 0 and args.mode == "encode":
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and args.mode == "encode":  # rank 0 at N=1 only
         cpu = cpu_baseline(args, np, torch, d_in, d_out, per, L)
-    if rank == 0 and args.cpu_sample > 0 and args.mode == "commit":
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and args.mode == "commit":
         cpu = cpu_baseline_commit(args, d_out, per, g.slice_len, L)
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -411,12 +411,21 @@ def cpu_baseline_commit(args, d_out, per, slice_len, L):
             "sample": f"{k} x 4 MiB objects' 20 slices, {threads} threads, one object per thread (hashlib SHA-256)"}
 
 
+def copy_share(args, world: int) -> int:
+    """Objects per rank in the copy-inclusive legs: the whole share on one GPU (config 5's
+    per-GPU share when --objects 2048); 256 per rank at N > 1, where every rank's pinned in/out
+    buffers (18.5 MB per object) share the node's host memory and PCIe."""
+    if args.copy_objects >= 0:
+        return min(args.copy_objects, args.objects)
+    return args.objects if world == 1 else min(args.objects, 256)
+
+
 def copy_inclusive(args, torch, dist, world, slicer, batch, d_in, d_out, per, L, dev):
     """Copy-inclusive encode rate: pinned host object bytes in, pinned host
     slices out, through te_encode_batch_host (3-slot H2D / kernel / D2H pipeline).  Reported
     beside `value`, never as it.  Every rank runs it at once (max over ranks), so at N>1 it
     includes the host-memory / PCIe contention of the node."""
-    m = args.objects if args.copy_objects < 0 else min(args.copy_objects, args.objects)
+    m = copy_share(args, world)
     h_in = torch.empty(m * L, dtype=torch.uint8).pin_memory()
     h_in.copy_(d_in[:m * L])
     h_out = torch.empty(m * per, dtype=torch.uint8).pin_memory()
@@ -459,7 +468,7 @@ def copy_inclusive_commit(args, torch, dist, world, slicer, batch, d_in, d_out, 
     332-362), through te_encode_commit_batch_host: pinned object bytes in; slices, leaf hashes,
     roots and proofs out.  Per window size: the leaf kernel's parallelism is one lane per slice,
     so larger windows hash more slices at once."""
-    m = args.objects if args.copy_objects < 0 else min(args.copy_objects, args.objects)
+    m = copy_share(args, world)
     N, H = 20, 5
     h_in = torch.empty(m * L, dtype=torch.uint8).pin_memory()
     h_in.copy_(d_in[:m * L])
