@@ -63,6 +63,9 @@ constexpr uint32_t kDrop = 0x80000000u;    // offset past every resource: the ra
 #define TEC_DMA_ORDER 1   // 1: a step's stores are issued before the next plane's DMA (B1 waits vmcnt(0));
                           // 0: DMA first, B1 waits vmcnt(2) (measured 3 % slower)
 #endif
+#ifndef TEC_DMA_STORE_MASK
+#define TEC_DMA_STORE_MASK 1  // per-job chunk filter (te_recover_batch_device); 0: timing builds only
+#endif
 #ifndef TEC_DMA_ABLATE
 #define TEC_DMA_ABLATE 0  // timing builds only (scripts/kbench.hip): bit0 no stores, bit1 no DMA,
 #endif                    // bit2 trivial MDS, bit3 no vmcnt wait at B1, bit4 no B2 barrier
@@ -397,7 +400,7 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
                     d1[q] = *reinterpret_cast<const u32x4 *>(row + lo1);
                     const uint32_t node = (it >> 8) & 0xffu, tz0 = (it >> 16) & 0xffu, ts = it >> 24;
                     dst[q] = slice_off(node) + ((tz0 == 0xffu ? z0 : tz0) * kQ + (ts == 0xffu ? s : ts)) * sc;
-                    if (!((store_mask >> node) & 1u)) dst[q] = kDrop;  // a chunk the caller does not keep
+                    if (TEC_DMA_STORE_MASK && !((store_mask >> node) & 1u)) dst[q] = kDrop;  // a chunk the caller does not keep
                 }
             }
             // B1: the next plane's DMA has landed (this wave's pieces are older than its last
@@ -425,7 +428,7 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
         const u32x4 e0 = *reinterpret_cast<const u32x4 *>(row + lo0);
         const u32x4 e1 = *reinterpret_cast<const u32x4 *>(row + lo1);
         const uint32_t node = (it >> 8) & 0xffu, tz0 = (it >> 16) & 0xffu, ts = it >> 24;
-        const uint32_t d = ((store_mask >> node) & 1u)
+        const uint32_t d = (!TEC_DMA_STORE_MASK || ((store_mask >> node) & 1u))
                                ? slice_off(node) + ((tz0 == 0xffu ? kQ - 1u : tz0) * kQ + (ts == 0xffu ? kQ - 1u : ts)) * sc
                                : kDrop;
         if (!(TEC_DMA_ABLATE & 1)) {
