@@ -56,6 +56,27 @@ class OuterCoder:
         return bytes(out)[:self._k * cb]
 
 
+class ReedSolomonCoder(OuterCoder):
+    """ReedSolomonCoder (lib/slicer/src/reed_solomon.rs:17-181): the Basic profile's coder
+    ("testing/debugging only", reed_solomon.rs:10-13) -- the same GF(2^16) codec with
+    (k data, m parity) and a slice-size ceiling (MAX_SLICE_BYTES = 4 KiB by default)."""
+
+    MAX_SLICE_BYTES = 1 << 12  # reed_solomon.rs:13
+
+    def __init__(self, k: int, m: int, max_slice_bytes: int = MAX_SLICE_BYTES):
+        assert k > 0, "k must be > 0"                      # reed_solomon.rs:38-40
+        assert m > 0, "m must be > 0"
+        assert max_slice_bytes > 0, "max_slice_bytes must be > 0"
+        assert k + m <= 65536, "too many total slices for RS field"
+        super().__init__(k, k + m)
+        self.max_slice_bytes = max_slice_bytes
+
+    def encode(self, data: bytes) -> list[bytes]:
+        if int(lib.te_outer_chunk_bytes(self._k, len(data))) > self.max_slice_bytes:
+            raise EncodeError("TooMuchData")               # reed_solomon.rs:85-87
+        return super().encode(data)
+
+
 def encode_device(k: int, m: int, d_in, chunk_bytes: int, segments: int, seg_in: int, d_out, seg_out: int,
                   stream=None) -> None:
     """te_outer_encode_device: `segments` OuterCoder encodes on device buffers (torch tensors)."""
@@ -65,4 +86,4 @@ def encode_device(k: int, m: int, d_in, chunk_bytes: int, segments: int, seg_in:
     _check(r, "encode")
 
 
-__all__ = ["OuterCoder", "encode_device", "MAX_CHUNK_BYTES", "EncodeError", "DecodeError", "_lib"]
+__all__ = ["OuterCoder", "ReedSolomonCoder", "encode_device", "MAX_CHUNK_BYTES", "EncodeError", "DecodeError", "_lib"]

@@ -84,3 +84,32 @@ def test_encode_device_segments():
         shards = [host[(g * k + j) * cb:(g * k + j + 1) * cb].tobytes() for j in range(k)]
         exp = b"".join(rs16.encode(k, m, shards))
         assert got[g * m * cb:(g + 1) * m * cb].tobytes() == exp, g
+
+
+# ---- ReedSolomonCoder (lib/slicer/src/reed_solomon.rs:182-351, k = 10, m = 10) ----
+def _rs():
+    from tape_amd.outer import ReedSolomonCoder
+    return ReedSolomonCoder(10, 10)
+
+
+def test_rs_coder_reference_tests():
+    c = _rs()
+    o = rs16.OracleOuter(10, 20)
+    for sz in (1, 9, 10, 11, 20, 5_000, 20_000, 30_000):  # test_many_sizes
+        d = make_data(sz)
+        ch = c.encode(d)
+        assert ch == o.encode(d) and len(ch) == 20 and len({len(x) for x in ch}) == 1
+        assert c.decode(list(enumerate(ch))[:10])[:sz] == d
+    ch = list(enumerate(c.encode(make_data(20_000))))
+    assert c.decode(ch)[:20_000] == make_data(20_000)                        # test_roundtrip_all
+    assert c.decode([x for x in ch if x[0] % 2 == 0])[:20_000] == make_data(20_000)  # mixed
+    assert c.decode(ch[10:])[:20_000] == make_data(20_000)                   # parity only
+    with pytest.raises(T.DecodeError):
+        c.decode(ch[:9])                                                     # test_insufficient
+    bad = [(i, x[:-1] if i == 0 else x) for i, x in ch]
+    with pytest.raises(T.DecodeError):
+        c.decode(bad)                                                        # test_size_mismatch
+    e = list(enumerate(c.encode(b"")))                                       # test_empty
+    assert len(e) == 20 and not any(c.decode(e[10:]))
+    with pytest.raises(T.EncodeError):
+        c.encode(bytes(10 * 4096 + 1))                                       # past MAX_SLICE_BYTES
