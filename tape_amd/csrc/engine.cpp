@@ -760,7 +760,12 @@ const te_clay::DecCache *dec_pattern(te_clay *c, uint64_t emask) {
         auto cost = [](const DecProgHdr &x) {
             return (decode_stage_rows(x.nslots, x.max_out) > 53 ? 1u << 20 : 0u) + x.nscratch;
         };
+        static const int force = [] {  // TEC_DEC_ORIENT=0/1: one row orientation only (measurement)
+            const char *e = getenv("TEC_DEC_ORIENT");
+            return e ? atoi(e) : -1;
+        }();
         for (int orient = 0; orient < 2; orient++) {
+            if (force >= 0 && orient != force) continue;
             DecProgHdr H;
             std::vector<DecStep> st;
             if (!h.dec_prog(d.P, orient, H, st) || !decode_stage_fits(H.nslots, H.max_out)) continue;
