@@ -788,7 +788,7 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     const ClayHost &h = c->h;
     const int n = h.n;
     const int rotated = (cfg && !raw) ? cfg->rotated : 0;
-    if (c->dec_cache.size() > 8192) c->dec_cache.clear();  // bounded (77,520 masks exist for k = 7)
+    if (c->dec_cache.size() > 1024) c->dec_cache.clear();  // <= ~27 MB (26 KB per pattern; 77,520 masks exist for k = 7)
     std::map<uint64_t, uint32_t> pat_index;  // erased mask -> pattern id
     std::vector<GpePattern> pats;
     std::vector<const te_clay::DecCache *> cached;
