@@ -88,12 +88,14 @@ def dist_setup(torch, dist, backend: str):
 KERNELS = {
     "encode": ["tec::dma::enc_dma_kernel<false>"],
     "repair": ["tec::rfold::rep_fold_kernel<0, 6>", "tec::rfold::rep_fold_kernel<1, 6>"],
-    "decode": ["tec::dstage::dec_stage_kernel<7, 6>"],
+    "decode": ["tec_dec_fixed"],  # the pattern kernels (dec_rtc.cpp); --decode-jit off: dec_stage_kernel<7, 6>
     "commit": ["tec::commit::leaf_kernel", "tec::commit::tree_kernel"],
 }
 
 
-def kernel_names(mode: str) -> list:
+def kernel_names(mode: str, decode_jit: str = "async") -> list:
+    if mode == "decode" and decode_jit == "off":
+        return ["tec::dstage::dec_stage_kernel<7, 6>"]
     return KERNELS.get(mode, [])
 
 
@@ -127,6 +129,9 @@ def main():
                     help="objects in the copy-inclusive (pinned host -> host) leg, encode mode "
                          "(-1 = the whole per-GPU share, 0 = skip)")
     ap.add_argument("--copy-steps", type=int, default=2)
+    ap.add_argument("--decode-jit", choices=["async", "off"], default="async",
+                    help="decode / recover: per-pattern decode kernels (hipRTC-built during warm-up) or "
+                         "the table-driven kernel only")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -219,6 +224,23 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    jit = None
+    if args.mode in ("decode", "recover"):
+        # hot patterns' kernels compile on worker threads from the first decode on (one per
+        # stripe rotation here); wait for them, then warm up again: one-time work, untimed
+        if args.decode_jit == "off":
+            slicer.coder.set_decode_jit("off")
+        t_jit = time.perf_counter()
+        ready, pending, failed = slicer.coder.decode_jit_status()
+        while pending:
+            ready, pending, failed = slicer.coder.decode_jit_status(timeout_ms=30_000)
+            print(f"[bench] pattern kernels: {ready} ready, {pending} compiling, {failed} failed "
+                  f"({time.perf_counter() - t_jit:.0f} s)", file=sys.stderr, flush=True)
+        jit = {"mode": args.decode_jit, "ready": ready, "failed": failed,
+               "compile_wait_s": round(time.perf_counter() - t_jit, 1)}
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -292,7 +314,7 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json)).get(args.mode, {})  # per mode (scripts/traffic.py)
-            if tj.get("objects") == nobj and tj.get("kernels") == kernel_names(args.mode):
+            if tj.get("objects") == nobj and tj.get("kernels") == kernel_names(args.mode, args.decode_jit):
                 traffic = tj.get("hbm_bytes_per_step")
         except Exception:
             traffic = None
@@ -331,6 +353,8 @@ def main():
             "commit_GiBps_vs_objects": commit_sweep,
             "outputs_verified": verified,
         }
+        if jit is not None:
+            line["decode_jit"] = jit
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -356,6 +380,23 @@ def outer_bench(args, torch, dist, world, rank, dev):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    jit = None
+    if args.mode in ("decode", "recover"):
+        # hot patterns' kernels compile on worker threads from the first decode on (one per
+        # stripe rotation here); wait for them, then warm up again: one-time work, untimed
+        if args.decode_jit == "off":
+            slicer.coder.set_decode_jit("off")
+        t_jit = time.perf_counter()
+        ready, pending, failed = slicer.coder.decode_jit_status()
+        while pending:
+            ready, pending, failed = slicer.coder.decode_jit_status(timeout_ms=30_000)
+            print(f"[bench] pattern kernels: {ready} ready, {pending} compiling, {failed} failed "
+                  f"({time.perf_counter() - t_jit:.0f} s)", file=sys.stderr, flush=True)
+        jit = {"mode": args.decode_jit, "ready": ready, "failed": failed,
+               "compile_wait_s": round(time.perf_counter() - t_jit, 1)}
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     batch.kernel_time_ms()

@@ -101,6 +101,17 @@ void te_clay_free(te_clay *c);
  * is restored on return).  Re-binding drains and frees the handle's device state first. */
 int te_clay_bind_device(te_clay *c, int device);
 int te_clay_device(const te_clay *c);
+/* Per-pattern decode kernels (no reference counterpart; an engine knob).  A hot erasure pattern
+ * of a q = 10, t = 2 profile gets a kernel with its plane program and decoding matrix compiled
+ * in (hipRTC, ~25 s of host time, off the caller's thread in mode 1); until then, and for every
+ * other pattern, the table-driven kernel decodes it.  mode: 0 off, 1 async (default; env
+ * TEC_DEC_JIT=off|sync|async), 2 sync (compile in the decoding call).  A pattern is built once
+ * `min_stripes` of its stripes have been decoded on the handle (default 1024, env
+ * TEC_DEC_JIT_MIN). */
+int te_clay_set_decode_jit(te_clay *c, int mode, uint64_t min_stripes);
+/* Pattern kernels ready / compiling / failed on the handle, after waiting up to `timeout_ms` for
+ * compiles in flight to finish. */
+int te_clay_decode_jit_status(te_clay *c, uint32_t timeout_ms, uint32_t *ready, uint32_t *pending, uint32_t *failed);
 int te_clay_get_info(const te_clay *c, te_clay_info *out);
 /* ClayCoder::chunk_size_for  clay.rs:61-73 */
 size_t te_clay_chunk_size_for(const te_clay *c, size_t input_len);

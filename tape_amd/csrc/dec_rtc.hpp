@@ -1,0 +1,169 @@
+// dec_rtc.hpp -- host side of the per-pattern decode kernels (dec_fixed.hpp): one erasure
+// pattern's plane program (ClayHost::dec_prog) written out as the straight-line source of the
+// kernel `tec_dec_fixed`, which engine.cpp compiles with hipRTC.
+#pragma once
+#include <algorithm>
+#include <cstdio>
+#include <string>
+#include <vector>
+#include "kernels.hpp"
+
+namespace tec {
+
+constexpr const char *kDecFixedKernel = "tec_dec_fixed";
+
+// LDS bytes of a pattern's kernel: two staging buffers of max_out rows, then the slots
+inline size_t dec_fixed_lds(const DecProgHdr &H, int G) { return (size_t)(2 * H.max_out + H.nslots) * G * 256u; }
+
+// The kernel source for known nodes P.known, decoding matrix D[e][j] (GF(2^8) coefficients of
+// erased e over known j), the unpacked steps of dec_prog, G waves per workgroup, and the type-1
+// coefficient t_u (C = t_u (U ^ Cp) ^ Cp).
+inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpeMaxKnown], const DecProgHdr &H,
+                                    const std::vector<DecStep> &steps, int G, uint8_t t_u) {
+    const int NK = (int)P.nknown, NE = (int)P.nerased, NS = (int)steps.size();
+    const uint32_t MO = H.max_out, SLOT0 = 2 * MO;
+    std::string s;
+    char b[256];
+    auto emit = [&](const char *fmt, auto... v) {
+        snprintf(b, sizeof b, fmt, v...);
+        s += b;
+    };
+    auto lty = [](uint32_t loc) { return loc >> 24; };
+    auto lix = [](uint32_t loc) { return loc & 0xffffffu; };
+    auto id2 = [](int a, int c) { return std::to_string(a) + "_" + std::to_string(c); };
+    s += "#include \"dec_fixed.hpp\"\nusing namespace tec::dfix;\n";
+    // flush items per step (data chunk x | plane << 8), scalar-loaded after each step's barrier
+    emit("__constant__ unsigned short kItems[%d][%d] = {\n", std::max(NS, 1), kDecMaxOut);
+    for (int st = 0; st < NS; st++) {
+        s += "{";
+        for (int r = 0; r < kDecMaxOut; r++)
+            emit("%u%s", r < (int)steps[st].nout ? steps[st].out[r] & 0xffffu : 0u, r + 1 < kDecMaxOut ? "," : "");
+        s += st + 1 < NS ? "},\n" : "}\n";
+    }
+    s += "};\n";
+    emit("extern \"C\" __global__ void __attribute__((amdgpu_flat_work_group_size(1, %d), amdgpu_waves_per_eu(4)))\n",
+         G * 64);
+    emit("%s(Args a) {\n  extern __shared__ __attribute__((aligned(16))) u32 lds[];\n", kDecFixedKernel);
+    emit("  const Tile<%d> T(a, reinterpret_cast<u8 *>(lds));\n", G);
+    // loads of step st: own rows, input partners, type-1 partners; then its scratch reads
+    auto loads = [&](int st) {
+        if (st >= NS) return;
+        const DecStep &S = steps[st];
+        for (int j = 0; j < NK; j++) {
+            emit("  const u32 o%s = T.ld(%u, %u);\n", id2(st, j).c_str(), (unsigned)H.knode[j], S.z);
+            if (S.kk[j] == kKnInput) emit("  const u32 p%s = T.ld(%u, %u);\n", id2(st, j).c_str(), S.kp[j] & 0xffu, S.kp[j] >> 8);
+        }
+        for (int e = 0; e < NE; e++)
+            if (S.ek[e] == kErType1) emit("  const u32 t%s = T.ld(%u, %u);\n", id2(st, e).c_str(), S.ep[e] & 0xffu, S.ep[e] >> 8);
+    };
+    auto scr_loads = [&](int st) {
+        if (st >= NS) return;
+        const DecStep &S = steps[st];
+        for (int j = 0; j < NK; j++)
+            if (S.kk[j] == kKnLoc && lty(S.kp[j]) == kLocScratch) emit("  const u32 q%s = T.scr_ld(%u);\n", id2(st, j).c_str(), lix(S.kp[j]));
+        for (int e = 0; e < NE; e++)
+            if (S.ek[e] == kErFinish && lty(S.ep[e]) == kLocScratch) emit("  const u32 r%s = T.scr_ld(%u);\n", id2(st, e).c_str(), lix(S.ep[e]));
+    };
+    loads(0);
+    scr_loads(0);
+    for (int st = 0; st < NS; st++) {
+        const DecStep &S = steps[st];
+        const uint32_t sb = (uint32_t)(st & 1) * MO;
+        auto put = [&](uint32_t loc, const std::string &v) {
+            if (loc == kLocNone) return;
+            if (lty(loc) == kLocStage) emit("  T.lds_st(%u, %s);\n", sb + lix(loc), v.c_str());
+            else if (lty(loc) == kLocSlot) emit("  T.lds_st(%u, %s);\n", SLOT0 + lix(loc), v.c_str());
+            else emit("  T.scr_st(%u, %s);\n", lix(loc), v.c_str());
+        };
+        emit("  // step %d: plane %u\n", st, S.z);
+        loads(st + 1);
+        // uncouple the known nodes; known data rows are staged as they are
+        for (int j = 0; j < NK; j++) {
+            const std::string id = id2(st, j);
+            const char *i = id.c_str();
+            emit("  const u32 c%s = T.rot(o%s);\n", i, i);
+            if (S.kk[j] == kKnRed) emit("  const u32 u%s = c%s;\n", i, i);
+            else if (S.kk[j] == kKnInput) emit("  const u32 u%s = pft3(c%s, T.rot(p%s));\n", i, i, i);
+            else if (lty(S.kp[j]) == kLocSlot) emit("  const u32 u%s = pft3(c%s, T.lds_ld(%u));\n", i, i, SLOT0 + lix(S.kp[j]));
+            else emit("  const u32 u%s = pft3(c%s, q%s);\n", i, i, i);
+            put(S.kout[j], "c" + id);
+        }
+        // pair partners' U, read before this step's writes (a location is reusable from its consumer on)
+        for (int e = 0; e < NE; e++) {
+            if (S.ek[e] != kErFinish) continue;
+            const std::string id = id2(st, e);
+            if (lty(S.ep[e]) == kLocSlot) emit("  const u32 v%s = T.lds_ld(%u);\n", id.c_str(), SLOT0 + lix(S.ep[e]));
+            else emit("  const u32 v%s = r%s;\n", id.c_str(), id.c_str());
+        }
+        // MDS: the erased U's this step needs, j-major over xtime multiples, XOR3 pairs
+        std::vector<std::string> acc(NE), pend(NE);
+        int tmp = 0;
+        for (int j = 0; j < NK; j++) {
+            int top = -1;
+            for (int e = 0; e < NE; e++)
+                if (S.ek[e] != kErSkip)
+                    for (int i = 0; i < 8; i++)
+                        if ((D[e][j] >> i) & 1) top = std::max(top, i);
+            if (top < 0) continue;
+            std::vector<std::string> m(top + 1);
+            m[0] = "u" + id2(st, j);
+            for (int i = 1; i <= top; i++) {
+                m[i] = "m" + id2(st, j) + "_" + std::to_string(i);
+                emit("  const u32 %s = xt(%s);\n", m[i].c_str(), m[i - 1].c_str());
+            }
+            for (int e = 0; e < NE; e++) {
+                if (S.ek[e] == kErSkip) continue;
+                for (int i = 0; i <= top; i++) {
+                    if (!((D[e][j] >> i) & 1)) continue;
+                    if (pend[e].empty()) { pend[e] = m[i]; continue; }
+                    const std::string nm = "x" + id2(st, tmp++);
+                    if (acc[e].empty()) emit("  const u32 %s = %s ^ %s;\n", nm.c_str(), pend[e].c_str(), m[i].c_str());
+                    else emit("  const u32 %s = xor3(%s, %s, %s);\n", nm.c_str(), acc[e].c_str(), pend[e].c_str(), m[i].c_str());
+                    acc[e] = nm;
+                    pend[e].clear();
+                }
+            }
+        }
+        for (int e = 0; e < NE; e++) {
+            if (S.ek[e] == kErSkip) continue;
+            const std::string nm = "a" + id2(st, e);
+            const std::string v = acc[e].empty() ? (pend[e].empty() ? "0u" : pend[e])
+                                                 : (pend[e].empty() ? acc[e] : acc[e] + " ^ " + pend[e]);
+            emit("  const u32 %s = %s;\n", nm.c_str(), v.c_str());
+        }
+        // results: staged data rows, parked / type-1 values in slots or scratch
+        for (int e = 0; e < NE; e++) {
+            const std::string id = id2(st, e), a = "a" + id;
+            const char *i = id.c_str();
+            switch (S.ek[e]) {
+                case kErRed: put(S.ed0[e], a); break;
+                case kErType1: {  // C = t_u (U ^ Cp) ^ Cp
+                    emit("  const u32 k%s = T.rot(t%s);\n", i, i);
+                    emit("  const u32 y%s_0 = %s ^ k%s;\n", i, a.c_str(), i);
+                    std::string r;
+                    for (int bit = 0; bit < 8 && (t_u >> bit); bit++) {
+                        if (bit) emit("  const u32 y%s_%d = xt(y%s_%d);\n", i, bit, i, bit - 1);
+                        if ((t_u >> bit) & 1) r += (r.empty() ? "" : " ^ ") + ("y" + id + "_" + std::to_string(bit));
+                    }
+                    emit("  const u32 w%s = %s ^ k%s;\n", i, r.empty() ? "0u" : r.c_str(), i);
+                    put(S.ed0[e], "w" + id);
+                    put(S.ed1[e], "w" + id);
+                    break;
+                }
+                case kErPark: put(S.ep[e], a); break;
+                case kErFinish:
+                    put(S.ed0[e], "pft3(" + a + ", v" + id + ")");
+                    put(S.epd[e], "pft3(v" + id + ", " + a + ")");
+                    break;
+                default: break;
+            }
+        }
+        scr_loads(st + 1);
+        s += "  T.barrier();\n";
+        emit("  T.flush(%u, kItems[%d], %u);\n", sb, st, S.nout);
+    }
+    s += "}\n";
+    return s;
+}
+
+}  // namespace tec

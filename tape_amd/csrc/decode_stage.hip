@@ -30,6 +30,9 @@ namespace dstage {
 #ifndef TEC_DEC_ST_AUX
 #define TEC_DEC_ST_AUX 2  // cache policy of the output row stores (2 = nt: ~1 % faster)
 #endif
+#ifndef TEC_DEC_COND_LD
+#define TEC_DEC_COND_LD 0  // 1: issue only the loads a step uses (uniform branches); 0: every slot, range-dropped
+#endif
 #ifndef TEC_DEC_WPE
 #define TEC_DEC_WPE 4  // waves per SIMD the register budget is cut for
 #endif
@@ -83,11 +86,14 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
     uint32_t kbase[NK];  // the known nodes' slices
 #pragma unroll
     for (int j = 0; j < NK; j++) kbase[j] = __builtin_amdgcn_readlane(sl_lane, H.knode[j]);
-    auto ldin = [&](uint32_t so) -> uint32_t {
+    // raw input word (the tail-word rotation is applied where the value is consumed, so a load
+    // inside a branch has no use inside it)
+    auto ldraw = [&](uint32_t so) -> uint32_t {
         if (TEC_DEC_ABLATE & 8) return so;
-        const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rs_in, (int)vcol, (int)so, 0);
-        return __builtin_amdgcn_alignbyte(v, v, vsh);
+        return __builtin_amdgcn_raw_buffer_load_b32(rs_in, (int)vcol, (int)so, 0);
     };
+    auto ldopt = [&](uint32_t so) -> uint32_t { return (TEC_DEC_COND_LD && so == 0x80000000u) ? 0u : ldraw(so); };
+    auto rot = [&](uint32_t v) { return __builtin_amdgcn_alignbyte(v, v, vsh); };
     // LDS rows: two staging buffers of max_out rows (a step stages into buffer st & 1, so one
     // barrier per step suffices), a zero row, a trash row, then the lane-private slots
     const uint32_t mo = H.max_out, zrow = 2u * mo, trow = zrow + 1u, srow0 = zrow + 2u;
@@ -159,11 +165,11 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
         const uint32_t vin = vec_in(x);
 #pragma unroll
         for (int j = 0; j < NK; j++) {
-            own[j] = ldin(kbase[j] + zs);
-            part[j] = ldin(W(vin, kDpKd + j));
+            own[j] = ldraw(kbase[j] + zs);
+            part[j] = ldopt(W(vin, kDpKd + j));
         }
 #pragma unroll
-        for (int e = 0; e < NE; e++) tkp[e] = ldin(W(vin, kDpEd + e));
+        for (int e = 0; e < NE; e++) tkp[e] = ldopt(W(vin, kDpEd + e));
     };
     // scratch loads of a step, issued after the previous step's scratch stores (lane-private
     // addresses: program order within the lane is the only ordering needed)
@@ -175,12 +181,14 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
             for (int e = 0; e < NE; e++) esc[e] = 0;
             return;
         }
+        auto ld = [&](uint32_t so) -> uint32_t {
+            return (TEC_DEC_COND_LD && so == 0x80000000u) ? 0u
+                                                          : __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)col_local, (int)so, 0);
+        };
 #pragma unroll
-        for (int j = 0; j < NK; j++)
-            ksc[j] = __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)col_local, (int)W(vs, kDpKd + j), 0);
+        for (int j = 0; j < NK; j++) ksc[j] = ld(W(vs, kDpKd + j));
 #pragma unroll
-        for (int e = 0; e < NE; e++)
-            esc[e] = __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)col_local, (int)W(vs, kDpEd + e), 0);
+        for (int e = 0; e < NE; e++) esc[e] = ld(W(vs, kDpEd + e));
     };
 
     const uint32_t nsteps = H.nsteps;
@@ -191,9 +199,9 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
         const uint32_t w_nn = ldw(st + 2);
         uint32_t cown[NK], cpart[NK], ctkp[NE];
 #pragma unroll
-        for (int j = 0; j < NK; j++) cown[j] = own[j], cpart[j] = part[j];
+        for (int j = 0; j < NK; j++) cown[j] = rot(own[j]), cpart[j] = rot(part[j]);
 #pragma unroll
-        for (int e = 0; e < NE; e++) ctkp[e] = tkp[e];
+        for (int e = 0; e < NE; e++) ctkp[e] = rot(tkp[e]);
         load_step(w_nxt);  // blank step: every partner load dropped
         if constexpr (TEC_DEC_PRIO) __builtin_amdgcn_s_setprio(TEC_DEC_PRIO);
         // ---- uncouple the known nodes: dropped loads read 0, a non-slot partner reads the zero
@@ -287,13 +295,13 @@ uint32_t decode_stage_rows(uint32_t nslots, uint32_t max_out) { return 2 * max_o
 bool decode_stage_fits(uint32_t nslots, uint32_t max_out) { return decode_stage_rows(nslots, max_out) <= dstage::kMaxLdsRows; }
 bool decode_stage_k(int k) { return k >= 7 && k <= 10; }
 
-static uint32_t dec_stage_g(uint32_t words_per_stripe) {
+uint32_t decode_stage_g(uint32_t words_per_stripe) {
     const uint32_t groups = (words_per_stripe + 63) / 64;
     return groups < (uint32_t)dstage::kMaxG ? groups : (uint32_t)dstage::kMaxG;
 }
 
 size_t decode_stage_scratch_bytes(const DecArgs &a) {
-    const uint32_t groups = (a.words_per_stripe + 63) / 64, g = dec_stage_g(a.words_per_stripe);
+    const uint32_t groups = (a.words_per_stripe + 63) / 64, g = decode_stage_g(a.words_per_stripe);
     const uint32_t wgs = (groups + g - 1) / g;
     return (size_t)a.njobs * wgs * (a.nscratch_max ? a.nscratch_max : 1) * g * 256u;
 }
@@ -329,7 +337,7 @@ hipError_t launch_decode_stage(DecArgs a, hipStream_t s) {
     if (a.lds_rows == 0 || a.lds_rows > dstage::kMaxLdsRows || a.sc < 8 || !a.scratch || a.n != 2u * kRepQ ||
         !decode_stage_k((int)a.nk))
         return hipErrorInvalidValue;
-    const uint32_t groups = (a.words_per_stripe + 63) / 64, g = dec_stage_g(a.words_per_stripe);
+    const uint32_t groups = (a.words_per_stripe + 63) / 64, g = decode_stage_g(a.words_per_stripe);
     a.wgs_per_stripe = (groups + g - 1) / g;
     const uint64_t blocks = (uint64_t)a.njobs * a.wgs_per_stripe;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;

@@ -268,7 +268,12 @@ struct te_clay {
         bool staged = false;           // a plane program exists for the staged kernel
         DecProgHdr H{};
         std::vector<DecStepP> steps;   // packed program + 2 blank steps
+        int orient = 0;                // the program's row orientation (ClayHost::dec_prog)
     };
+    // per-pattern decode kernels built at run time (dec_rtc.cpp); created on first decode
+    DecJit *jit = nullptr;
+    int jit_mode = -1;                 // te_clay_set_decode_jit; -1 = the environment's default
+    uint64_t jit_min = 0;
     std::unordered_map<uint64_t, DecCache> dec_cache;
     struct Slot {
         hipStream_t s = nullptr;
@@ -297,6 +302,8 @@ static void release_device_state(te_clay *c) {
     c->rec_slices.release();
     if (c->rec_done) (void)hipEventDestroy(c->rec_done);
     c->rec_done = nullptr;
+    dec_jit_free(c->jit);  // joins compiles in flight; every stream is drained above
+    c->jit = nullptr;
     c->rec_pending = false;
     if (c->stream) (void)hipStreamDestroy(c->stream);
     c->stream = nullptr;
@@ -415,6 +422,30 @@ int te_clay_bind_device(te_clay *c, int device) {
 }
 
 int te_clay_device(const te_clay *c) { return c ? c->device : -1; }
+
+int te_clay_set_decode_jit(te_clay *c, int mode, uint64_t min_stripes) {
+    if (!c || mode < 0 || mode > 2) return TE_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->jit_mode = mode;
+    c->jit_min = min_stripes;
+    if (c->jit) dec_jit_set(c->jit, mode, min_stripes);
+    return TE_OK;
+}
+
+int te_clay_decode_jit_status(te_clay *c, uint32_t timeout_ms, uint32_t *ready, uint32_t *pending, uint32_t *failed) {
+    if (!c) return TE_ERR_INVALID_ARG;
+    DecJit *j;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        j = c->jit;
+    }
+    uint32_t r = 0, p = 0, f = 0;
+    if (j) dec_jit_counts(j, timeout_ms, &r, &p, &f);  // j lives until the handle is freed or re-bound
+    if (ready) *ready = r;
+    if (pending) *pending = p;
+    if (failed) *failed = f;
+    return TE_OK;
+}
 
 int te_clay_from_params(uint64_t p, te_clay **out) {
     return te_clay_new((uint32_t)(p & 0xFF), (uint32_t)((p >> 8) & 0xFF), (uint32_t)((p >> 16) & 0xFF), out);
@@ -769,7 +800,7 @@ const te_clay::DecCache *dec_pattern(te_clay *c, uint64_t emask) {
             DecProgHdr H;
             std::vector<DecStep> st;
             if (!h.dec_prog(d.P, orient, H, st) || !decode_stage_fits(H.nslots, H.max_out)) continue;
-            if (!found || cost(H) < cost(best)) { best = H; best_steps.swap(st); found = true; }
+            if (!found || cost(H) < cost(best)) { best = H; best_steps.swap(st); found = true; d.orient = orient; }
         }
         bool ok = found;
         for (const DecStep &S : best_steps) {
@@ -851,6 +882,43 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         nscr_max = std::max(nscr_max, dc.H.nscratch);
     }
     lds_rows = std::max(lds_rows, 1u);
+    // the staged kernel addresses a stripe's slices and its output share with 31-bit offsets
+    auto staged_group = [&](uint64_t key) {
+        const uint64_t cs = key >> 32, sc = cs / (uint64_t)h.alpha;
+        return staged && sc >= 8 && (uint64_t)n * group_in_stride[key] < 0x7fffffffull &&
+               cs * (uint64_t)h.k < 0x7fffffffull;
+    };
+    // patterns with a per-pattern kernel built (dec_rtc.cpp) leave their group for a launch of
+    // their own; every staged stripe counts toward building its pattern's kernel
+    struct Fixed { uint64_t key; const DecJitKernel *k; std::vector<GpeJob> jobs; size_t off = 0; };
+    std::vector<Fixed> fixed;
+    if (staged) {
+        if (!c->jit) {
+            c->jit = dec_jit_new(c->device);
+            if (c->jit_mode >= 0) dec_jit_set(c->jit, c->jit_mode, c->jit_min);
+        }
+        for (auto &kv : groups) {
+            if (!staged_group(kv.first)) continue;
+            const uint32_t sc = (uint32_t)((kv.first >> 32) / (uint64_t)h.alpha);
+            const int G = (int)decode_stage_g((sc + 3) / 4);
+            std::vector<uint64_t> cnt(pats.size(), 0);
+            for (const GpeJob &g : kv.second) cnt[g.pattern]++;
+            std::vector<int> fx(pats.size(), -1);
+            for (size_t p = 0; p < pats.size(); p++) {
+                if (!cnt[p]) continue;
+                const DecJitKernel *k = dec_jit_get(c->jit, h, cached[p]->P, cached[p]->orient, G, cnt[p]);
+                if (!k) continue;
+                fx[p] = (int)fixed.size();
+                fixed.push_back(Fixed{kv.first, k, {}});
+            }
+            std::vector<GpeJob> rest;
+            for (const GpeJob &g : kv.second) {
+                if (fx[g.pattern] >= 0) fixed[fx[g.pattern]].jobs.push_back(g);
+                else rest.push_back(g);
+            }
+            kv.second.swap(rest);
+        }
+    }
     Arena &A = c->dec;
     A.img.clear();
     const size_t pat_off = A.put(pats.data(), pats.size() * sizeof(GpePattern));
@@ -862,15 +930,11 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         soff_off = A.put(dstep_off.data(), dstep_off.size() * sizeof(uint32_t));
     }
     std::vector<std::pair<uint64_t, size_t>> offs;
-    for (auto &kv : groups) offs.push_back({kv.first, A.put(kv.second.data(), kv.second.size() * sizeof(GpeJob))});
+    for (auto &kv : groups)
+        if (!kv.second.empty()) offs.push_back({kv.first, A.put(kv.second.data(), kv.second.size() * sizeof(GpeJob))});
+    for (Fixed &f : fixed) f.off = A.put(f.jobs.data(), f.jobs.size() * sizeof(GpeJob));
     int r = A.upload(s);
     if (r) return r;
-    // the staged kernel addresses a stripe's slices and its output share with 31-bit offsets
-    auto staged_group = [&](uint64_t key) {
-        const uint64_t cs = key >> 32, sc = cs / (uint64_t)h.alpha;
-        return staged && sc >= 8 && (uint64_t)n * group_in_stride[key] < 0x7fffffffull &&
-               cs * (uint64_t)h.k < 0x7fffffffull;
-    };
     auto dec_args = [&](const std::pair<uint64_t, size_t> &o) {
         const uint64_t cs = o.first >> 32;
         const uint32_t sc = (uint32_t)(cs / (uint64_t)h.alpha);
@@ -889,15 +953,40 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         a.out_stride = cs;
         return a;
     };
+    auto fixed_args = [&](const Fixed &f, uint8_t *scratch) {
+        const uint64_t cs = f.key >> 32;
+        dfix_args a{};
+        a.jobs = reinterpret_cast<const dfix::Job *>(A.at<GpeJob>(f.off));
+        a.scratch = scratch;
+        a.in_stride = group_in_stride[f.key];
+        a.out_stride = cs;
+        a.njobs = (uint32_t)f.jobs.size();
+        a.sc = (uint32_t)(cs / (uint64_t)h.alpha);
+        a.wps = (a.sc + 3) / 4;
+        const uint32_t groups_ = (a.wps + 63) / 64, G = decode_stage_g(a.wps);
+        a.wgs_per_stripe = (groups_ + G - 1) / G;
+        a.n = (uint32_t)n;
+        a.nscratch = f.k->nscratch;
+        return a;
+    };
     size_t scratch_bytes = 0;
     for (auto &o : offs)
         if (staged_group(o.first)) scratch_bytes = std::max(scratch_bytes, decode_stage_scratch_bytes(dec_args(o)));
+    for (const Fixed &f : fixed) {
+        const dfix_args a = fixed_args(f, nullptr);
+        const size_t b = (size_t)a.njobs * a.wgs_per_stripe * std::max(a.nscratch, 1u) * decode_stage_g(a.wps) * 256u;
+        scratch_bytes = std::max(scratch_bytes, b);
+    }
     uint8_t *scratch = nullptr;
     if (scratch_bytes) {
         r = A.workspace(scratch_bytes, s, &scratch);
         if (r) return r;
     }
     KTimer kt(s);
+    for (const Fixed &f : fixed) {
+        const dfix_args a = fixed_args(f, scratch);
+        TE_HIP(launch_dec_fixed(*f.k, a, decode_stage_g(a.wps), s));
+    }
     for (auto &o : offs) {
         if (staged_group(o.first)) {
             DecArgs a = dec_args(o);

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "gf.hpp"
+#include "dec_fixed.hpp"
 
 namespace tec {
 
@@ -186,6 +187,25 @@ hipError_t launch_decode_stage(DecArgs a, hipStream_t s);
 size_t decode_stage_scratch_bytes(const DecArgs &a);
 uint32_t decode_stage_rows(uint32_t nslots, uint32_t max_out);  // LDS rows of a program
 bool decode_stage_fits(uint32_t nslots, uint32_t max_out);
+uint32_t decode_stage_g(uint32_t words_per_stripe);             // waves per workgroup
+
+// Per-pattern decode kernels compiled at run time (dec_rtc.cpp, dec_fixed.hpp), per handle.
+using dfix_args = dfix::Args;
+static_assert(sizeof(dfix::Job) == sizeof(GpeJob) && offsetof(dfix::Job, rot) == offsetof(GpeJob, rot), "dfix::Job");
+struct DecJitKernel {
+    hipFunction_t fn;
+    size_t lds;          // dynamic LDS bytes
+    uint32_t nscratch;   // scratch rows per tile
+};
+struct DecJit;
+struct ClayHost;
+DecJit *dec_jit_new(int device);
+void dec_jit_free(DecJit *j);
+void dec_jit_set(DecJit *j, int mode, uint64_t min_stripes);  // mode 0 off, 1 async, 2 sync
+void dec_jit_counts(DecJit *j, uint32_t timeout_ms, uint32_t *ready, uint32_t *pending, uint32_t *failed);
+// The pattern's kernel for G waves if built; counts `stripes` toward building it.
+const DecJitKernel *dec_jit_get(DecJit *j, const ClayHost &h, const GpePattern &P, int orient, int G, uint64_t stripes);
+hipError_t launch_dec_fixed(const DecJitKernel &k, const dfix_args &a, uint32_t G, hipStream_t s);
 bool decode_stage_k(int k);  // a staged-decode kernel is compiled for this k (n = 20)
 
 // ---- slice commitments (commit.hip) ----

@@ -276,6 +276,21 @@ class ClayCoder:
     def device(self) -> int:
         return int(lib.te_clay_device(self._h))
 
+    def set_decode_jit(self, mode: str = "async", min_stripes: int = 1024) -> None:
+        """te_clay_set_decode_jit: per-pattern decode kernels off / built in the background /
+        built in the decoding call, once a pattern has decoded `min_stripes` stripes."""
+        r = lib.te_clay_set_decode_jit(self._h, {"off": 0, "async": 1, "sync": 2}[mode], min_stripes)
+        if r:
+            raise _engine_error(r)
+
+    def decode_jit_status(self, timeout_ms: int = 0) -> tuple:
+        """(ready, compiling, failed) per-pattern kernels, after waiting up to timeout_ms."""
+        v = [C.c_uint32(0) for _ in range(3)]
+        r = lib.te_clay_decode_jit_status(self._h, timeout_ms, *[C.byref(x) for x in v])
+        if r:
+            raise _engine_error(r)
+        return tuple(int(x.value) for x in v)
+
     def k(self) -> int:
         return self._info.k
 
