@@ -101,6 +101,18 @@ template <int G> struct Tile {
     TEC_DFI void scr_st(u32 row, u32 v) const {
         __builtin_amdgcn_raw_buffer_store_b32(v, rs_scr, (int)col_local, (int)(row * RS), 0);
     }
+    // one decoded word straight to data chunk x at plane z: every lane stores the dword it
+    // loaded at (vcol; a tail lane's rotation undone: its 4 columns are col - 2 .. col + 1, two
+    // of them duplicates of its neighbour's, same values); a dword across the stripe's output
+    // share is written byte by byte (the range check drops whole accesses)
+    TEC_DFI void out_st(u32 x, u32 z, u32 v) const {
+        const u32 o = x * out_stride + z * sc + vcol, w = rot(v);
+        if (o + 4u > olen && o < olen) {
+            for (u32 k = 0; k < 4u; k++) __builtin_amdgcn_raw_buffer_store_b8((u8)(w >> (8u * k)), rs_out, (int)(o + k), 0, 0);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b32(w, rs_out, (int)o, 0, 2);
+        }
+    }
     TEC_DFI void barrier() const { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
     // this wave's share [wv n / G, (wv + 1) n / G) of the step's n staged rows -> data chunk x

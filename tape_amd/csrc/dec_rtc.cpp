@@ -96,7 +96,12 @@ void dec_jit_counts(DecJit *j, uint32_t timeout_ms, uint32_t *ready, uint32_t *p
     if (failed) *failed = f;
 }
 
-static void compile(DecJit *j, Entry *E, std::string src, size_t lds, uint32_t nscratch) {
+static void compile(DecJit *j, Entry *E, std::string src, size_t lds, uint32_t nscratch, bool queued) {
+    if (queued) {  // a worker: at most kMaxCompiles compile at once
+        std::unique_lock<std::mutex> g(j->mu);
+        j->cv.wait(g, [&] { return j->running < kMaxCompiles; });
+        j->running++;
+    }
     std::string err;
     hiprtcProgram prog = nullptr;
     const char *hdrs[] = {kDecFixedHeader};
@@ -156,7 +161,7 @@ const DecJitKernel *dec_jit_get(DecJit *j, const ClayHost &h, const GpePattern &
         E = j->ents.emplace(key, std::make_unique<Entry>()).first->second.get();
     }
     E->seen += stripes;
-    if (E->seen < j->min_stripes || (j->mode == 1 && j->running >= kMaxCompiles)) return nullptr;
+    if (E->seen < j->min_stripes) return nullptr;
     // the pattern's program and matrix, as dec_pattern compiled them
     DecProgHdr H;
     std::vector<DecStep> steps;
@@ -170,16 +175,20 @@ const DecJitKernel *dec_jit_get(DecJit *j, const ClayHost &h, const GpePattern &
     uint8_t D[kGpeMaxErased][kGpeMaxKnown] = {};
     for (size_t e = 0; e < erased.size(); e++)
         for (size_t k = 0; k < known.size(); k++) D[e][k] = Dm.v[e][k];
-    std::string src = dec_fixed_source(P, D, H, steps, G, kPft.t_u[0]);
-    const size_t lds = dec_fixed_lds(H, G);
+    static const bool direct = [] {  // TEC_DEC_JIT_OUT=stage: rows staged in LDS, flushed whole (measurement)
+        const char *e = getenv("TEC_DEC_JIT_OUT");
+        return !(e && !strcmp(e, "stage"));
+    }();
+    std::string src = dec_fixed_source(P, D, H, steps, G, kPft.t_u[0], direct);
+    const size_t lds = dec_fixed_lds(H, G, direct);
     E->state.store(1);
-    j->running++;
     if (j->mode == 2) {
+        j->running++;
         g.unlock();
-        compile(j, E, std::move(src), lds, H.nscratch);
+        compile(j, E, std::move(src), lds, H.nscratch, false);
         return E->state.load() == 2 ? &E->k : nullptr;
     }
-    j->threads.emplace_back(compile, j, E, std::move(src), lds, H.nscratch);
+    j->threads.emplace_back(compile, j, E, std::move(src), lds, H.nscratch, true);
     return nullptr;
 }
 

@@ -13,15 +13,17 @@ namespace tec {
 constexpr const char *kDecFixedKernel = "tec_dec_fixed";
 
 // LDS bytes of a pattern's kernel: two staging buffers of max_out rows, then the slots
-inline size_t dec_fixed_lds(const DecProgHdr &H, int G) { return (size_t)(2 * H.max_out + H.nslots) * G * 256u; }
+inline size_t dec_fixed_lds(const DecProgHdr &H, int G, bool direct) {
+    return (size_t)((direct ? 0 : 2 * H.max_out) + H.nslots) * G * 256u;
+}
 
 // The kernel source for known nodes P.known, decoding matrix D[e][j] (GF(2^8) coefficients of
 // erased e over known j), the unpacked steps of dec_prog, G waves per workgroup, and the type-1
 // coefficient t_u (C = t_u (U ^ Cp) ^ Cp).
 inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpeMaxKnown], const DecProgHdr &H,
-                                    const std::vector<DecStep> &steps, int G, uint8_t t_u) {
+                                    const std::vector<DecStep> &steps, int G, uint8_t t_u, bool direct) {
     const int NK = (int)P.nknown, NE = (int)P.nerased, NS = (int)steps.size();
-    const uint32_t MO = H.max_out, SLOT0 = 2 * MO;
+    const uint32_t MO = H.max_out, SLOT0 = direct ? 0 : 2 * MO;
     std::string s;
     char b[256];
     auto emit = [&](const char *fmt, auto... v) {
@@ -33,14 +35,14 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
     auto id2 = [](int a, int c) { return std::to_string(a) + "_" + std::to_string(c); };
     s += "#include \"dec_fixed.hpp\"\nusing namespace tec::dfix;\n";
     // flush items per step (data chunk x | plane << 8), scalar-loaded after each step's barrier
-    emit("__constant__ unsigned short kItems[%d][%d] = {\n", std::max(NS, 1), kDecMaxOut);
-    for (int st = 0; st < NS; st++) {
+    if (!direct) emit("__constant__ unsigned short kItems[%d][%d] = {\n", std::max(NS, 1), kDecMaxOut);
+    for (int st = 0; st < NS && !direct; st++) {
         s += "{";
         for (int r = 0; r < kDecMaxOut; r++)
             emit("%u%s", r < (int)steps[st].nout ? steps[st].out[r] & 0xffffu : 0u, r + 1 < kDecMaxOut ? "," : "");
         s += st + 1 < NS ? "},\n" : "}\n";
     }
-    s += "};\n";
+    if (!direct) s += "};\n";
     emit("extern \"C\" __global__ void __attribute__((amdgpu_flat_work_group_size(1, %d), amdgpu_waves_per_eu(4)))\n",
          G * 64);
     emit("%s(Args a) {\n  extern __shared__ __attribute__((aligned(16))) u32 lds[];\n", kDecFixedKernel);
@@ -71,7 +73,9 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
         const uint32_t sb = (uint32_t)(st & 1) * MO;
         auto put = [&](uint32_t loc, const std::string &v) {
             if (loc == kLocNone) return;
-            if (lty(loc) == kLocStage) emit("  T.lds_st(%u, %s);\n", sb + lix(loc), v.c_str());
+            if (lty(loc) == kLocStage && direct)
+                emit("  T.out_st(%u, %u, %s);\n", S.out[lix(loc)] & 0xffu, (S.out[lix(loc)] >> 8) & 0xffu, v.c_str());
+            else if (lty(loc) == kLocStage) emit("  T.lds_st(%u, %s);\n", sb + lix(loc), v.c_str());
             else if (lty(loc) == kLocSlot) emit("  T.lds_st(%u, %s);\n", SLOT0 + lix(loc), v.c_str());
             else emit("  T.scr_st(%u, %s);\n", lix(loc), v.c_str());
         };
@@ -159,8 +163,10 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
             }
         }
         scr_loads(st + 1);
-        s += "  T.barrier();\n";
-        emit("  T.flush(%u, kItems[%d], %u);\n", sb, st, S.nout);
+        if (!direct) {  // staged rows: flushed whole after the step's barrier
+            s += "  T.barrier();\n";
+            emit("  T.flush(%u, kItems[%d], %u);\n", sb, st, S.nout);
+        }
     }
     s += "}\n";
     return s;
