@@ -49,9 +49,52 @@ TEC_DFI u32 xt(u32 x) {
 }
 TEC_DFI u32 pft3(u32 a, u32 b) { return a ^ xt(a ^ b); }  // 3a ^ 2b: U from (C, C_partner), C from (U, U_partner)
 
-// Per-lane state of a workgroup's tile: one stripe's row segment, G waves x 64 lanes x 4 columns.
-template <int G> struct Tile {
-    static constexpr u32 RS = G * 256u;  // LDS row stride
+// A lane's 8 columns (8-byte lanes, WB = 8): two dwords, every operation byte-wise per dword.
+struct V2 {
+    u32 x, y;
+};
+TEC_DFI V2 operator^(V2 a, V2 b) { return V2{a.x ^ b.x, a.y ^ b.y}; }
+TEC_DFI V2 xor3(V2 a, V2 b, V2 c) { return V2{xor3(a.x, b.x, c.x), xor3(a.y, b.y, c.y)}; }
+TEC_DFI V2 xt(V2 a) { return V2{xt(a.x), xt(a.y)}; }
+TEC_DFI V2 pft3(V2 a, V2 b) { return a ^ xt(a ^ b); }
+
+// Lane value type and its memory forms per lane width.
+template <int WB> struct Lane;
+template <> struct Lane<4> {
+    typedef u32 V;
+    static TEC_DFI V zero() { return 0u; }
+    static TEC_DFI V ld(__amdgpu_buffer_rsrc_t r, u32 vo, u32 so) { return __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo, (int)so, 0); }
+    template <int AUX> static TEC_DFI void st(V v, __amdgpu_buffer_rsrc_t r, u32 vo, u32 so) { __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)vo, (int)so, AUX); }
+    // bytes [s, 4) then [0, s): the tail lane's columns from a load s bytes early
+    static TEC_DFI V rot(V v, u32 s) { return __builtin_amdgcn_alignbyte(v, v, s); }
+    static TEC_DFI V unrot(V v, u32 s) { return __builtin_amdgcn_alignbyte(v, v, (4u - s) & 3u); }
+    static TEC_DFI u32 byte(V v, u32 k) { return v >> (8u * k); }
+};
+template <> struct Lane<8> {
+    typedef V2 V;
+    typedef u32 u32x2 __attribute__((ext_vector_type(2)));
+    static TEC_DFI V zero() { return V2{0u, 0u}; }
+    static TEC_DFI V ld(__amdgpu_buffer_rsrc_t r, u32 vo, u32 so) {
+        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(r, (int)vo, (int)so, 0);
+        return V2{t.x, t.y};
+    }
+    template <int AUX> static TEC_DFI void st(V v, __amdgpu_buffer_rsrc_t r, u32 vo, u32 so) {
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, r, (int)vo, (int)so, AUX);
+    }
+    // rotate the 8 bytes right by s (even, < 8): byte i <- byte (i + s) mod 8
+    static TEC_DFI V rot(V v, u32 s) {
+        const bool sw = s >= 4u;
+        const u32 a = sw ? v.y : v.x, b = sw ? v.x : v.y, t = s & 3u;
+        return V2{__builtin_amdgcn_alignbyte(b, a, t), __builtin_amdgcn_alignbyte(a, b, t)};
+    }
+    static TEC_DFI V unrot(V v, u32 s) { return rot(v, (8u - s) & 7u); }
+    static TEC_DFI u32 byte(V v, u32 k) { return (k < 4u ? v.x : v.y) >> (8u * (k & 3u)); }
+};
+
+// Per-lane state of a workgroup's tile: one stripe's row segment, G waves x 64 lanes x WB columns.
+template <int G, int WB = 4> struct Tile {
+    typedef typename Lane<WB>::V V;
+    static constexpr u32 RS = G * 64u * WB;  // LDS row stride
     u8 *lds8;
     u32 wv, lane, col_local, vcol, vsh, sc, seg0, lseg, nb, tail, olen;
     bool wide_tail;
@@ -63,7 +106,7 @@ template <int G> struct Tile {
         lds8 = lds;
         wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         lane = threadIdx.x & 63u;
-        col_local = threadIdx.x * 4u;
+        col_local = threadIdx.x * (u32)WB;
         const u32 nbk = gridDim.x, b = blockIdx.x, full = nbk & ~7u;  // XCD-contiguous tiles (dev_io.hpp xcd_tile)
         const u32 tile = b >= full ? b : (b & 7u) * (full >> 3) + (b >> 3);
         const u32 job = tile / a.wgs_per_stripe, seg = tile - job * a.wgs_per_stripe;
@@ -74,10 +117,11 @@ template <int G> struct Tile {
         lseg = a.sc - seg0 < RS ? a.sc - seg0 : RS;
         u32 w = seg * G * 64u + threadIdx.x;
         if (w >= a.wps) w = a.wps - 1;
-        const u32 col = w * 4u;
-        const bool tailw = col + 4u > a.sc;  // the word's high half is past the sub-chunk: load 2 B early
-        vcol = tailw ? col - 2u : col;
-        vsh = tailw ? 2u : 0u;
+        const u32 col = w * (u32)WB;
+        // the word's high part is past the sub-chunk: load the row's last WB bytes instead
+        const bool tailw = col + WB > a.sc;
+        vcol = tailw ? a.sc - WB : col;
+        vsh = col - vcol;
         rs_in = __builtin_amdgcn_make_buffer_rsrc((void *)J.in, 0, (int)(u32)(a.n * a.in_stride), 0x00020000);
         rs_out = __builtin_amdgcn_make_buffer_rsrc((void *)J.out, 0, (int)(u32)J.out_len, 0x00020000);
         const u32 nscr = a.nscratch ? a.nscratch : 1u;
@@ -91,26 +135,23 @@ template <int G> struct Tile {
         wide_tail = tail != 0 && nb > 0;
         olen = (u32)J.out_len;
     }
-    TEC_DFI u32 ld(u32 node, u32 plane) const {
-        return __builtin_amdgcn_raw_buffer_load_b32(rs_in, (int)vcol, (int)(nbase[node] + plane * sc), 0);
-    }
-    TEC_DFI u32 rot(u32 v) const { return __builtin_amdgcn_alignbyte(v, v, vsh); }
-    TEC_DFI u32 lds_ld(u32 row) const { return *reinterpret_cast<const u32 *>(lds8 + row * RS + col_local); }
-    TEC_DFI void lds_st(u32 row, u32 v) const { *reinterpret_cast<u32 *>(lds8 + row * RS + col_local) = v; }
-    TEC_DFI u32 scr_ld(u32 row) const { return __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)col_local, (int)(row * RS), 0); }
-    TEC_DFI void scr_st(u32 row, u32 v) const {
-        __builtin_amdgcn_raw_buffer_store_b32(v, rs_scr, (int)col_local, (int)(row * RS), 0);
-    }
-    // one decoded word straight to data chunk x at plane z: every lane stores the dword it
-    // loaded at (vcol; a tail lane's rotation undone: its 4 columns are col - 2 .. col + 1, two
-    // of them duplicates of its neighbour's, same values); a dword across the stripe's output
-    // share is written byte by byte (the range check drops whole accesses)
-    TEC_DFI void out_st(u32 x, u32 z, u32 v) const {
-        const u32 o = x * out_stride + z * sc + vcol, w = rot(v);
-        if (o + 4u > olen && o < olen) {
-            for (u32 k = 0; k < 4u; k++) __builtin_amdgcn_raw_buffer_store_b8((u8)(w >> (8u * k)), rs_out, (int)(o + k), 0, 0);
+    TEC_DFI V ld(u32 node, u32 plane) const { return Lane<WB>::ld(rs_in, vcol, nbase[node] + plane * sc); }
+    TEC_DFI V rot(V v) const { return Lane<WB>::rot(v, vsh); }
+    TEC_DFI V lds_ld(u32 row) const { return *reinterpret_cast<const V *>(lds8 + row * RS + col_local); }
+    TEC_DFI void lds_st(u32 row, V v) const { *reinterpret_cast<V *>(lds8 + row * RS + col_local) = v; }
+    TEC_DFI V scr_ld(u32 row) const { return Lane<WB>::ld(rs_scr, col_local, row * RS); }
+    TEC_DFI void scr_st(u32 row, V v) const { Lane<WB>::template st<0>(v, rs_scr, col_local, row * RS); }
+    // one decoded word straight to data chunk x at plane z: every lane stores the bytes it
+    // loaded at (vcol; a tail lane's rotation undone: its columns overlap its neighbour's, same
+    // values); a word across the stripe's output share is written byte by byte (the range check
+    // drops whole dwords)
+    TEC_DFI void out_st(u32 x, u32 z, V v) const {
+        const u32 o = x * out_stride + z * sc + vcol;
+        const V w = Lane<WB>::unrot(v, vsh);
+        if (o + (u32)WB > olen && o < olen) {
+            for (u32 k = 0; k < (u32)WB; k++) __builtin_amdgcn_raw_buffer_store_b8((u8)Lane<WB>::byte(w, k), rs_out, (int)(o + k), 0, 0);
         } else {
-            __builtin_amdgcn_raw_buffer_store_b32(w, rs_out, (int)o, 0, 2);
+            Lane<WB>::template st<2>(w, rs_out, o, 0);
         }
     }
     TEC_DFI void barrier() const { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }

@@ -18,6 +18,7 @@
 #include <thread>
 #include <vector>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include "kernels.hpp"
 #include "clay_host.hpp"
@@ -96,7 +97,24 @@ void dec_jit_counts(DecJit *j, uint32_t timeout_ms, uint32_t *ready, uint32_t *p
     if (failed) *failed = f;
 }
 
-static void compile(DecJit *j, Entry *E, std::string src, size_t lds, uint32_t nscratch, bool queued) {
+DecJitGeom dec_jit_geom(uint32_t sc) {
+    // 8-column lanes (TEC_DEC_JIT_WB=8) halve the memory instructions per byte but measured the
+    // same on one box (4.71-4.72 vs 4.67-4.71 ms per 1024 x 4 MiB worst-case step) and compile
+    // twice as long, so 4-column lanes are the default
+    static const uint32_t wb_env = [] {
+        const char *e = getenv("TEC_DEC_JIT_WB");
+        return e && !strcmp(e, "8") ? 8u : 4u;
+    }();
+    DecJitGeom g{};
+    g.wb = sc >= 64u ? wb_env : 4u;
+    g.wps = (sc + g.wb - 1) / g.wb;
+    const uint32_t groups = (g.wps + 63) / 64;
+    g.G = g.wb == 8u ? std::min(groups, 6u) : decode_stage_g((sc + 3) / 4);
+    g.wgs = (groups + g.G - 1) / g.G;
+    return g;
+}
+
+static void compile(DecJit *j, Entry *E, std::string src, size_t lds, uint32_t nscratch, uint32_t wb, bool queued) {
     if (queued) {  // a worker: at most kMaxCompiles compile at once
         std::unique_lock<std::mutex> g(j->mu);
         j->cv.wait(g, [&] { return j->running < kMaxCompiles; });
@@ -138,6 +156,7 @@ static void compile(DecJit *j, Entry *E, std::string src, size_t lds, uint32_t n
         E->k.fn = fn;
         E->k.lds = lds;
         E->k.nscratch = nscratch;
+        E->k.wb = wb;
         E->state.store(2);
     } else {
         if (mod) (void)hipModuleUnload(mod);
@@ -148,9 +167,9 @@ static void compile(DecJit *j, Entry *E, std::string src, size_t lds, uint32_t n
     j->cv.notify_all();
 }
 
-const DecJitKernel *dec_jit_get(DecJit *j, const ClayHost &h, const GpePattern &P, int orient, int G, uint64_t stripes) {
-    if (!j || P.erased_mask >> 32 || G < 1 || G > 6) return nullptr;
-    const uint64_t key = P.erased_mask | (uint64_t)G << 32;
+const DecJitKernel *dec_jit_get(DecJit *j, const ClayHost &h, const GpePattern &P, int orient, int G, int wb, uint64_t stripes) {
+    if (!j || P.erased_mask >> 32 || G < 1 || G > 6 || (wb != 4 && wb != 8)) return nullptr;
+    const uint64_t key = P.erased_mask | (uint64_t)G << 32 | (uint64_t)wb << 40;
     std::unique_lock<std::mutex> g(j->mu);
     auto f = j->ents.find(key);
     Entry *E = f == j->ents.end() ? nullptr : f->second.get();
@@ -179,16 +198,17 @@ const DecJitKernel *dec_jit_get(DecJit *j, const ClayHost &h, const GpePattern &
         const char *e = getenv("TEC_DEC_JIT_OUT");
         return !(e && !strcmp(e, "stage"));
     }();
-    std::string src = dec_fixed_source(P, D, H, steps, G, kPft.t_u[0], direct);
-    const size_t lds = dec_fixed_lds(H, G, direct);
+    if (!direct) wb = 4;  // the staged form (measurement only) has 4-column lanes
+    std::string src = dec_fixed_source(P, D, H, steps, G, kPft.t_u[0], direct, wb);
+    const size_t lds = dec_fixed_lds(H, G, direct, wb);
     E->state.store(1);
     if (j->mode == 2) {
         j->running++;
         g.unlock();
-        compile(j, E, std::move(src), lds, H.nscratch, false);
+        compile(j, E, std::move(src), lds, H.nscratch, (uint32_t)wb, false);
         return E->state.load() == 2 ? &E->k : nullptr;
     }
-    j->threads.emplace_back(compile, j, E, std::move(src), lds, H.nscratch, true);
+    j->threads.emplace_back(compile, j, E, std::move(src), lds, H.nscratch, (uint32_t)wb, true);
     return nullptr;
 }
 

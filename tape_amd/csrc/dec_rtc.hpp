@@ -4,6 +4,7 @@
 #pragma once
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 #include "kernels.hpp"
@@ -12,16 +13,27 @@ namespace tec {
 
 constexpr const char *kDecFixedKernel = "tec_dec_fixed";
 
-// LDS bytes of a pattern's kernel: two staging buffers of max_out rows, then the slots
-inline size_t dec_fixed_lds(const DecProgHdr &H, int G, bool direct) {
-    return (size_t)((direct ? 0 : 2 * H.max_out) + H.nslots) * G * 256u;
+// waves per SIMD the 8-column kernels are compiled for (TEC_DEC_JIT_WPE, measurement knob)
+inline int dec_fixed_wpe8() {
+    static const int w = [] {
+        const char *e = getenv("TEC_DEC_JIT_WPE");
+        const int v = e ? atoi(e) : 3;  // 3: 4.78 ms; 2: 5.34; 4: spills, 7.88 (1024 x 4 MiB, 13 erasures)
+        return v >= 1 && v <= 8 ? v : 3;
+    }();
+    return w;
+}
+
+// LDS bytes of a pattern's kernel: two staging buffers of max_out rows, then the slots (rows of
+// G waves x 64 lanes x wb bytes)
+inline size_t dec_fixed_lds(const DecProgHdr &H, int G, bool direct, int wb) {
+    return (size_t)((direct ? 0 : 2 * H.max_out) + H.nslots) * G * 64u * (uint32_t)wb;
 }
 
 // The kernel source for known nodes P.known, decoding matrix D[e][j] (GF(2^8) coefficients of
 // erased e over known j), the unpacked steps of dec_prog, G waves per workgroup, and the type-1
-// coefficient t_u (C = t_u (U ^ Cp) ^ Cp).
+// coefficient t_u (C = t_u (U ^ Cp) ^ Cp), wb columns per lane (4, or 8 for direct output).
 inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpeMaxKnown], const DecProgHdr &H,
-                                    const std::vector<DecStep> &steps, int G, uint8_t t_u, bool direct) {
+                                    const std::vector<DecStep> &steps, int G, uint8_t t_u, bool direct, int wb) {
     const int NK = (int)P.nknown, NE = (int)P.nerased, NS = (int)steps.size();
     const uint32_t MO = H.max_out, SLOT0 = direct ? 0 : 2 * MO;
     std::string s;
@@ -34,6 +46,7 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
     auto lix = [](uint32_t loc) { return loc & 0xffffffu; };
     auto id2 = [](int a, int c) { return std::to_string(a) + "_" + std::to_string(c); };
     s += "#include \"dec_fixed.hpp\"\nusing namespace tec::dfix;\n";
+    emit("typedef Lane<%d>::V VT;\n#define VZ (Lane<%d>::zero())\n", wb, wb);
     // flush items per step (data chunk x | plane << 8), scalar-loaded after each step's barrier
     if (!direct) emit("__constant__ unsigned short kItems[%d][%d] = {\n", std::max(NS, 1), kDecMaxOut);
     for (int st = 0; st < NS && !direct; st++) {
@@ -43,28 +56,28 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
         s += st + 1 < NS ? "},\n" : "}\n";
     }
     if (!direct) s += "};\n";
-    emit("extern \"C\" __global__ void __attribute__((amdgpu_flat_work_group_size(1, %d), amdgpu_waves_per_eu(4)))\n",
-         G * 64);
+    emit("extern \"C\" __global__ void __attribute__((amdgpu_flat_work_group_size(1, %d), amdgpu_waves_per_eu(%d)))\n",
+         G * 64, wb == 8 ? dec_fixed_wpe8() : 4);
     emit("%s(Args a) {\n  extern __shared__ __attribute__((aligned(16))) u32 lds[];\n", kDecFixedKernel);
-    emit("  const Tile<%d> T(a, reinterpret_cast<u8 *>(lds));\n", G);
+    emit("  const Tile<%d, %d> T(a, reinterpret_cast<u8 *>(lds));\n", G, wb);
     // loads of step st: own rows, input partners, type-1 partners; then its scratch reads
     auto loads = [&](int st) {
         if (st >= NS) return;
         const DecStep &S = steps[st];
         for (int j = 0; j < NK; j++) {
-            emit("  const u32 o%s = T.ld(%u, %u);\n", id2(st, j).c_str(), (unsigned)H.knode[j], S.z);
-            if (S.kk[j] == kKnInput) emit("  const u32 p%s = T.ld(%u, %u);\n", id2(st, j).c_str(), S.kp[j] & 0xffu, S.kp[j] >> 8);
+            emit("  const VT o%s = T.ld(%u, %u);\n", id2(st, j).c_str(), (unsigned)H.knode[j], S.z);
+            if (S.kk[j] == kKnInput) emit("  const VT p%s = T.ld(%u, %u);\n", id2(st, j).c_str(), S.kp[j] & 0xffu, S.kp[j] >> 8);
         }
         for (int e = 0; e < NE; e++)
-            if (S.ek[e] == kErType1) emit("  const u32 t%s = T.ld(%u, %u);\n", id2(st, e).c_str(), S.ep[e] & 0xffu, S.ep[e] >> 8);
+            if (S.ek[e] == kErType1) emit("  const VT t%s = T.ld(%u, %u);\n", id2(st, e).c_str(), S.ep[e] & 0xffu, S.ep[e] >> 8);
     };
     auto scr_loads = [&](int st) {
         if (st >= NS) return;
         const DecStep &S = steps[st];
         for (int j = 0; j < NK; j++)
-            if (S.kk[j] == kKnLoc && lty(S.kp[j]) == kLocScratch) emit("  const u32 q%s = T.scr_ld(%u);\n", id2(st, j).c_str(), lix(S.kp[j]));
+            if (S.kk[j] == kKnLoc && lty(S.kp[j]) == kLocScratch) emit("  const VT q%s = T.scr_ld(%u);\n", id2(st, j).c_str(), lix(S.kp[j]));
         for (int e = 0; e < NE; e++)
-            if (S.ek[e] == kErFinish && lty(S.ep[e]) == kLocScratch) emit("  const u32 r%s = T.scr_ld(%u);\n", id2(st, e).c_str(), lix(S.ep[e]));
+            if (S.ek[e] == kErFinish && lty(S.ep[e]) == kLocScratch) emit("  const VT r%s = T.scr_ld(%u);\n", id2(st, e).c_str(), lix(S.ep[e]));
     };
     loads(0);
     scr_loads(0);
@@ -85,19 +98,19 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
         for (int j = 0; j < NK; j++) {
             const std::string id = id2(st, j);
             const char *i = id.c_str();
-            emit("  const u32 c%s = T.rot(o%s);\n", i, i);
-            if (S.kk[j] == kKnRed) emit("  const u32 u%s = c%s;\n", i, i);
-            else if (S.kk[j] == kKnInput) emit("  const u32 u%s = pft3(c%s, T.rot(p%s));\n", i, i, i);
-            else if (lty(S.kp[j]) == kLocSlot) emit("  const u32 u%s = pft3(c%s, T.lds_ld(%u));\n", i, i, SLOT0 + lix(S.kp[j]));
-            else emit("  const u32 u%s = pft3(c%s, q%s);\n", i, i, i);
+            emit("  const VT c%s = T.rot(o%s);\n", i, i);
+            if (S.kk[j] == kKnRed) emit("  const VT u%s = c%s;\n", i, i);
+            else if (S.kk[j] == kKnInput) emit("  const VT u%s = pft3(c%s, T.rot(p%s));\n", i, i, i);
+            else if (lty(S.kp[j]) == kLocSlot) emit("  const VT u%s = pft3(c%s, T.lds_ld(%u));\n", i, i, SLOT0 + lix(S.kp[j]));
+            else emit("  const VT u%s = pft3(c%s, q%s);\n", i, i, i);
             put(S.kout[j], "c" + id);
         }
         // pair partners' U, read before this step's writes (a location is reusable from its consumer on)
         for (int e = 0; e < NE; e++) {
             if (S.ek[e] != kErFinish) continue;
             const std::string id = id2(st, e);
-            if (lty(S.ep[e]) == kLocSlot) emit("  const u32 v%s = T.lds_ld(%u);\n", id.c_str(), SLOT0 + lix(S.ep[e]));
-            else emit("  const u32 v%s = r%s;\n", id.c_str(), id.c_str());
+            if (lty(S.ep[e]) == kLocSlot) emit("  const VT v%s = T.lds_ld(%u);\n", id.c_str(), SLOT0 + lix(S.ep[e]));
+            else emit("  const VT v%s = r%s;\n", id.c_str(), id.c_str());
         }
         // MDS: the erased U's this step needs, j-major over xtime multiples, XOR3 pairs
         std::vector<std::string> acc(NE), pend(NE);
@@ -113,7 +126,7 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
             m[0] = "u" + id2(st, j);
             for (int i = 1; i <= top; i++) {
                 m[i] = "m" + id2(st, j) + "_" + std::to_string(i);
-                emit("  const u32 %s = xt(%s);\n", m[i].c_str(), m[i - 1].c_str());
+                emit("  const VT %s = xt(%s);\n", m[i].c_str(), m[i - 1].c_str());
             }
             for (int e = 0; e < NE; e++) {
                 if (S.ek[e] == kErSkip) continue;
@@ -121,8 +134,8 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
                     if (!((D[e][j] >> i) & 1)) continue;
                     if (pend[e].empty()) { pend[e] = m[i]; continue; }
                     const std::string nm = "x" + id2(st, tmp++);
-                    if (acc[e].empty()) emit("  const u32 %s = %s ^ %s;\n", nm.c_str(), pend[e].c_str(), m[i].c_str());
-                    else emit("  const u32 %s = xor3(%s, %s, %s);\n", nm.c_str(), acc[e].c_str(), pend[e].c_str(), m[i].c_str());
+                    if (acc[e].empty()) emit("  const VT %s = %s ^ %s;\n", nm.c_str(), pend[e].c_str(), m[i].c_str());
+                    else emit("  const VT %s = xor3(%s, %s, %s);\n", nm.c_str(), acc[e].c_str(), pend[e].c_str(), m[i].c_str());
                     acc[e] = nm;
                     pend[e].clear();
                 }
@@ -131,9 +144,9 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
         for (int e = 0; e < NE; e++) {
             if (S.ek[e] == kErSkip) continue;
             const std::string nm = "a" + id2(st, e);
-            const std::string v = acc[e].empty() ? (pend[e].empty() ? "0u" : pend[e])
+            const std::string v = acc[e].empty() ? (pend[e].empty() ? "VZ" : pend[e])
                                                  : (pend[e].empty() ? acc[e] : acc[e] + " ^ " + pend[e]);
-            emit("  const u32 %s = %s;\n", nm.c_str(), v.c_str());
+            emit("  const VT %s = %s;\n", nm.c_str(), v.c_str());
         }
         // results: staged data rows, parked / type-1 values in slots or scratch
         for (int e = 0; e < NE; e++) {
@@ -142,14 +155,14 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
             switch (S.ek[e]) {
                 case kErRed: put(S.ed0[e], a); break;
                 case kErType1: {  // C = t_u (U ^ Cp) ^ Cp
-                    emit("  const u32 k%s = T.rot(t%s);\n", i, i);
-                    emit("  const u32 y%s_0 = %s ^ k%s;\n", i, a.c_str(), i);
+                    emit("  const VT k%s = T.rot(t%s);\n", i, i);
+                    emit("  const VT y%s_0 = %s ^ k%s;\n", i, a.c_str(), i);
                     std::string r;
                     for (int bit = 0; bit < 8 && (t_u >> bit); bit++) {
-                        if (bit) emit("  const u32 y%s_%d = xt(y%s_%d);\n", i, bit, i, bit - 1);
+                        if (bit) emit("  const VT y%s_%d = xt(y%s_%d);\n", i, bit, i, bit - 1);
                         if ((t_u >> bit) & 1) r += (r.empty() ? "" : " ^ ") + ("y" + id + "_" + std::to_string(bit));
                     }
-                    emit("  const u32 w%s = %s ^ k%s;\n", i, r.empty() ? "0u" : r.c_str(), i);
+                    emit("  const VT w%s = %s ^ k%s;\n", i, r.empty() ? "VZ" : r.c_str(), i);
                     put(S.ed0[e], "w" + id);
                     put(S.ed1[e], "w" + id);
                     break;

@@ -900,13 +900,13 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         for (auto &kv : groups) {
             if (!staged_group(kv.first)) continue;
             const uint32_t sc = (uint32_t)((kv.first >> 32) / (uint64_t)h.alpha);
-            const int G = (int)decode_stage_g((sc + 3) / 4);
+            const DecJitGeom geo = dec_jit_geom(sc);
             std::vector<uint64_t> cnt(pats.size(), 0);
             for (const GpeJob &g : kv.second) cnt[g.pattern]++;
             std::vector<int> fx(pats.size(), -1);
             for (size_t p = 0; p < pats.size(); p++) {
                 if (!cnt[p]) continue;
-                const DecJitKernel *k = dec_jit_get(c->jit, h, cached[p]->P, cached[p]->orient, G, cnt[p]);
+                const DecJitKernel *k = dec_jit_get(c->jit, h, cached[p]->P, cached[p]->orient, (int)geo.G, (int)geo.wb, cnt[p]);
                 if (!k) continue;
                 fx[p] = (int)fixed.size();
                 fixed.push_back(Fixed{kv.first, k, {}});
@@ -962,9 +962,9 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         a.out_stride = cs;
         a.njobs = (uint32_t)f.jobs.size();
         a.sc = (uint32_t)(cs / (uint64_t)h.alpha);
-        a.wps = (a.sc + 3) / 4;
-        const uint32_t groups_ = (a.wps + 63) / 64, G = decode_stage_g(a.wps);
-        a.wgs_per_stripe = (groups_ + G - 1) / G;
+        const DecJitGeom geo = dec_jit_geom(a.sc);  // the geometry the kernel was built for
+        a.wps = geo.wps;
+        a.wgs_per_stripe = geo.wgs;
         a.n = (uint32_t)n;
         a.nscratch = f.k->nscratch;
         return a;
@@ -974,7 +974,8 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         if (staged_group(o.first)) scratch_bytes = std::max(scratch_bytes, decode_stage_scratch_bytes(dec_args(o)));
     for (const Fixed &f : fixed) {
         const dfix_args a = fixed_args(f, nullptr);
-        const size_t b = (size_t)a.njobs * a.wgs_per_stripe * std::max(a.nscratch, 1u) * decode_stage_g(a.wps) * 256u;
+        const DecJitGeom geo = dec_jit_geom(a.sc);
+        const size_t b = (size_t)a.njobs * a.wgs_per_stripe * std::max(a.nscratch, 1u) * geo.G * 64u * geo.wb;
         scratch_bytes = std::max(scratch_bytes, b);
     }
     uint8_t *scratch = nullptr;
@@ -985,7 +986,7 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     KTimer kt(s);
     for (const Fixed &f : fixed) {
         const dfix_args a = fixed_args(f, scratch);
-        TE_HIP(launch_dec_fixed(*f.k, a, decode_stage_g(a.wps), s));
+        TE_HIP(launch_dec_fixed(*f.k, a, dec_jit_geom(a.sc).G, s));
     }
     for (auto &o : offs) {
         if (staged_group(o.first)) {

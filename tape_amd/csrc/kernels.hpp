@@ -196,6 +196,7 @@ struct DecJitKernel {
     hipFunction_t fn;
     size_t lds;          // dynamic LDS bytes
     uint32_t nscratch;   // scratch rows per tile
+    uint32_t wb;         // columns per lane (4 or 8)
 };
 struct DecJit;
 struct ClayHost;
@@ -203,8 +204,12 @@ DecJit *dec_jit_new(int device);
 void dec_jit_free(DecJit *j);
 void dec_jit_set(DecJit *j, int mode, uint64_t min_stripes);  // mode 0 off, 1 async, 2 sync
 void dec_jit_counts(DecJit *j, uint32_t timeout_ms, uint32_t *ready, uint32_t *pending, uint32_t *failed);
-// The pattern's kernel for G waves if built; counts `stripes` toward building it.
-const DecJitKernel *dec_jit_get(DecJit *j, const ClayHost &h, const GpePattern &P, int orient, int G, uint64_t stripes);
+// The pattern's kernel for G waves of wb-column lanes if built; counts `stripes` toward building it.
+const DecJitKernel *dec_jit_get(DecJit *j, const ClayHost &h, const GpePattern &P, int orient, int G, int wb, uint64_t stripes);
+// Tile geometry of a pattern kernel for sub-chunk sc: lanes of wb columns, wps words per row,
+// G waves per workgroup, wgs workgroups per stripe.
+struct DecJitGeom { uint32_t wb, wps, G, wgs; };
+DecJitGeom dec_jit_geom(uint32_t sc);
 hipError_t launch_dec_fixed(const DecJitKernel &k, const dfix_args &a, uint32_t G, hipStream_t s);
 bool decode_stage_k(int k);  // a staged-decode kernel is compiled for this k (n = 20)
 
