@@ -109,7 +109,12 @@ DecJitGeom dec_jit_geom(uint32_t sc) {
     g.wb = sc >= 64u ? wb_env : 4u;
     g.wps = (sc + g.wb - 1) / g.wb;
     const uint32_t groups = (g.wps + 63) / 64;
-    g.G = g.wb == 8u ? std::min(groups, 6u) : decode_stage_g((sc + 3) / 4);
+    static const uint32_t g_env = [] {  // waves per workgroup (TEC_DEC_JIT_G, measurement knob)
+        const char *e = getenv("TEC_DEC_JIT_G");
+        const int v = e ? atoi(e) : 6;
+        return (uint32_t)(v >= 1 && v <= 6 ? v : 6);
+    }();
+    g.G = std::min(std::min(groups, 6u), g_env);
     g.wgs = (groups + g.G - 1) / g.G;
     return g;
 }

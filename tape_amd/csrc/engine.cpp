@@ -2,9 +2,10 @@
 //
 // Host side of the drop-in for lib/slicer: Slicer striping/padding/rotation/metadata
 // (slicer.rs, adaptive.rs, metadata.rs), repair planning (repair.rs), descriptor building and
-// launch orchestration.  All GF(2^8) arithmetic runs in the HIP kernels (encode_dma.hip,
-// encode_stage.hip, decode_stage.hip, repair_stage.hip, gpe.hip); there is no CPU compute fallback -- without a device the compute calls fail with
-// TE_ERR_NO_DEVICE.
+// launch orchestration.  All GF arithmetic and hashing runs in the HIP kernels (encode_dma.hip,
+// encode_stage.hip, decode_stage.hip + the per-pattern kernels of dec_rtc.cpp, repair_fold.hip,
+// repair_stage.hip, gpe.hip, commit.hip, rs16.hip); there is no CPU compute fallback -- without a
+// device the compute calls fail with TE_ERR_NO_DEVICE.
 #include <hip/hip_runtime.h>
 #include <string.h>
 #include <stdio.h>
