@@ -2046,7 +2046,7 @@ int te_outer_encode_device(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t
     if (device_count() <= 0) return TE_ERR_NO_DEVICE;
     const rs16::Tables &T = rs16::tables();
     const uint32_t c = rs16::chunk(k, m), span = rs16::skew_span(k, m), wl = rs16::work_len(k, m);
-    if ((size_t)span * 128 + (size_t)wl * 256 > 64 * 1024 || span > rs16::kModulus) return TE_ERR_UNSUPPORTED;
+    if ((size_t)span * 128 + (size_t)wl * 256 > 160 * 1024 || span > rs16::kModulus) return TE_ERR_UNSUPPORTED;
     // nibble tables of every skew multiplier the transforms touch (zeros for the basis' zero)
     std::vector<uint16_t> lut((size_t)span * 64, 0);
     for (uint32_t sx = 0; sx < span; sx++) {

@@ -10,6 +10,7 @@
 // of log_m = 65535, the basis' "zero", is all zeros, which makes the butterfly a plain XOR).
 // Decode applies the host-derived k x k decoding matrix the same way, one table per coefficient.
 // A first kernel: correct for every shard count the crate supports within the LDS budget.
+#include <algorithm>
 #include "kernels.hpp"
 
 namespace tec {
@@ -28,51 +29,73 @@ struct Col {  // one thread's work vector in LDS
     __device__ void st(uint32_t i, uint32_t v) const { w[i * bt] = (uint16_t)v; }
 };
 
-// FFT / IFFT of work[pos .. pos + size) (rs16.hpp restated on LDS columns)
+// FFT / IFFT of work[pos .. pos + size) (rs16.hpp restated on LDS columns).  A radix-4 group's
+// four values stay in registers across its four butterflies (4 LDS loads + 4 stores per group
+// instead of 8 + 8).
 __device__ void fft(const Col &c, const uint16_t *lut, uint32_t pos, uint32_t size, uint32_t trunc, uint32_t delta) {
-    auto b2 = [&](uint32_t ix, uint32_t iy, uint32_t s) {
-        uint32_t x = c.ld(pos + ix), y = c.ld(pos + iy);
-        x ^= mulx(y, lut + s * 64u);
-        y ^= x;
-        c.st(pos + ix, x);
-        c.st(pos + iy, y);
-    };
     uint32_t dist4 = size, dist = size >> 2;
     for (; dist; dist4 = dist, dist >>= 2)
         for (uint32_t r = 0; r < trunc; r += dist4) {
             const uint32_t b = r + dist + delta - 1;
+            const uint16_t *t0 = lut + b * 64u, *t1 = lut + (b + dist) * 64u, *t2 = lut + (b + 2 * dist) * 64u;
             for (uint32_t i = r; i < r + dist; i++) {
-                b2(i, i + 2 * dist, b + dist);
-                b2(i + dist, i + 3 * dist, b + dist);
-                b2(i, i + dist, b);
-                b2(i + 2 * dist, i + 3 * dist, b + 2 * dist);
+                const uint32_t p = pos + i;
+                uint32_t x0 = c.ld(p), x1 = c.ld(p + dist), x2 = c.ld(p + 2 * dist), x3 = c.ld(p + 3 * dist);
+                x0 ^= mulx(x2, t1);  // (i, i + 2 dist)
+                x2 ^= x0;
+                x1 ^= mulx(x3, t1);  // (i + dist, i + 3 dist)
+                x3 ^= x1;
+                x0 ^= mulx(x1, t0);  // (i, i + dist)
+                x1 ^= x0;
+                x2 ^= mulx(x3, t2);  // (i + 2 dist, i + 3 dist)
+                x3 ^= x2;
+                c.st(p, x0);
+                c.st(p + dist, x1);
+                c.st(p + 2 * dist, x2);
+                c.st(p + 3 * dist, x3);
             }
         }
     if (dist4 == 2)
-        for (uint32_t r = 0; r < trunc; r += 2) b2(r, r + 1, r + delta);
+        for (uint32_t r = 0; r < trunc; r += 2) {
+            uint32_t x = c.ld(pos + r), y = c.ld(pos + r + 1);
+            x ^= mulx(y, lut + (r + delta) * 64u);
+            y ^= x;
+            c.st(pos + r, x);
+            c.st(pos + r + 1, y);
+        }
 }
 
 __device__ void ifft(const Col &c, const uint16_t *lut, uint32_t pos, uint32_t size, uint32_t trunc, uint32_t delta) {
-    auto b2 = [&](uint32_t ix, uint32_t iy, uint32_t s) {
-        uint32_t x = c.ld(pos + ix), y = c.ld(pos + iy);
-        y ^= x;
-        x ^= mulx(y, lut + s * 64u);
-        c.st(pos + ix, x);
-        c.st(pos + iy, y);
-    };
     uint32_t dist = 1, dist4 = 4;
     for (; dist4 <= size; dist = dist4, dist4 <<= 2)
         for (uint32_t r = 0; r < trunc; r += dist4) {
             const uint32_t b = r + dist + delta - 1;
+            const uint16_t *t0 = lut + b * 64u, *t1 = lut + (b + dist) * 64u, *t2 = lut + (b + 2 * dist) * 64u;
             for (uint32_t i = r; i < r + dist; i++) {
-                b2(i, i + dist, b);
-                b2(i + 2 * dist, i + 3 * dist, b + 2 * dist);
-                b2(i, i + 2 * dist, b + dist);
-                b2(i + dist, i + 3 * dist, b + dist);
+                const uint32_t p = pos + i;
+                uint32_t x0 = c.ld(p), x1 = c.ld(p + dist), x2 = c.ld(p + 2 * dist), x3 = c.ld(p + 3 * dist);
+                x1 ^= x0;  // (i, i + dist)
+                x0 ^= mulx(x1, t0);
+                x3 ^= x2;  // (i + 2 dist, i + 3 dist)
+                x2 ^= mulx(x3, t2);
+                x2 ^= x0;  // (i, i + 2 dist)
+                x0 ^= mulx(x2, t1);
+                x3 ^= x1;  // (i + dist, i + 3 dist)
+                x1 ^= mulx(x3, t1);
+                c.st(p, x0);
+                c.st(p + dist, x1);
+                c.st(p + 2 * dist, x2);
+                c.st(p + 3 * dist, x3);
             }
         }
     if (dist < size)
-        for (uint32_t i = 0; i < dist; i++) b2(i, i + dist, dist + delta - 1);
+        for (uint32_t i = 0; i < dist; i++) {
+            uint32_t x = c.ld(i + pos), y = c.ld(i + dist + pos);
+            y ^= x;
+            x ^= mulx(y, lut + (dist + delta - 1) * 64u);
+            c.st(i + pos, x);
+            c.st(i + dist + pos, y);
+        }
 }
 
 __device__ __forceinline__ uint32_t ld_elem(const uint8_t *shard, uint32_t e) {
@@ -85,7 +108,7 @@ __device__ __forceinline__ void st_elem(uint8_t *shard, uint32_t e, uint32_t v) 
     shard[o + 32u] = (uint8_t)(v >> 8);
 }
 
-__global__ void __launch_bounds__(128) rs16_encode_kernel(Rs16EncArgs a) {  // grid.y = segments
+__global__ void __launch_bounds__(512) rs16_encode_kernel(Rs16EncArgs a) {  // grid.y = segments
     extern __shared__ __attribute__((aligned(16))) uint16_t lds16[];
     uint16_t *lut = lds16;                     // span x 64 entries
     uint16_t *work = lds16 + a.span * 64u;     // work_len x blockDim
@@ -146,11 +169,36 @@ __global__ void __launch_bounds__(128) rs16_decode_kernel(Rs16DecArgs a) {
 
 static uint32_t rs16_blocks(uint64_t elems) { return (uint32_t)((elems + 127) / 128); }
 
+// Block size of the encode: the nibble tables (span x 128 B) are staged once per block and every
+// thread keeps work_len u16 in LDS, so larger blocks amortise the tables; pick the size that
+// keeps the most waves per CU within its 160 KB of LDS (128 threads, 32.5 KB, for OuterCoder(17,
+// 50) left 8 waves per CU; 512 threads, 80.5 KB, leave 16).
+static uint32_t rs16_enc_threads(const Rs16EncArgs &a, size_t *lds_out) {
+    uint32_t best_t = 128, best_w = 0;
+    size_t best_lds = 0;
+    for (uint32_t t = 128; t <= 512; t *= 2) {
+        const size_t lds = (size_t)a.span * 128u + (size_t)a.work_len * t * 2u;
+        if (lds > 160 * 1024) break;
+        const uint32_t blocks = (uint32_t)((160 * 1024) / lds), waves = std::min(blocks * (t / 64u), 32u);
+        if (waves > best_w) { best_w = waves; best_t = t; best_lds = lds; }
+    }
+    *lds_out = best_lds;
+    return best_w ? best_t : 0;
+}
+
 hipError_t launch_rs16_encode(const Rs16EncArgs &a, uint32_t segments, hipStream_t s) {
     if (a.elems == 0 || segments == 0) return hipSuccess;
-    const size_t lds = (size_t)a.span * 128u + (size_t)a.work_len * 128u * 2u;
-    if (lds > 64 * 1024 || segments > 65535) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(rs16k::rs16_encode_kernel, dim3(rs16_blocks(a.elems), segments), dim3(128), lds, s, a);
+    size_t lds = 0;
+    const uint32_t t = rs16_enc_threads(a, &lds);
+    if (!t || segments > 65535) return hipErrorInvalidValue;
+    static size_t lds_set = 0;
+    if (lds > lds_set) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(rs16k::rs16_encode_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        lds_set = lds;
+    }
+    hipLaunchKernelGGL(rs16k::rs16_encode_kernel, dim3((uint32_t)((a.elems + t - 1) / t), segments), dim3(t), lds, s, a);
     return hipGetLastError();
 }
 
