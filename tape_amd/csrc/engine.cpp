@@ -2069,6 +2069,7 @@ int te_outer_encode_device(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t
         a.lut = d_lut;
         a.k = k; a.m = m; a.c = c; a.high = (uint32_t)rs16::use_high_rate(k, m);
         a.work_len = wl; a.span = span; a.elems = (uint32_t)(chunk_bytes / 2);
+        a.one_chunk = !a.high && c <= 32 && wl > c;
         KTimer kt(s);
         r = hip_status(launch_rs16_encode(a, segments, s));
         kt.stop();

@@ -247,6 +247,7 @@ struct Rs16EncArgs {
     uint64_t in_stride, out_stride, seg_in, seg_out;
     const uint16_t *lut;        // span x 64 nibble-table entries: multiplier = skew[s]
     uint32_t k, m, c, high, work_len, span, elems;  // elems: field elements per shard (bytes / 2)
+    uint32_t one_chunk;         // low rate, c <= 32: one chunk of work in LDS, the IFFT kept in registers
 };
 struct Rs16DecArgs {
     const uint8_t *const *recv; // k received shards (device pointer array)

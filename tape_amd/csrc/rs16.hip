@@ -108,7 +108,10 @@ __device__ __forceinline__ void st_elem(uint8_t *shard, uint32_t e, uint32_t v) 
     shard[o + 32u] = (uint8_t)(v >> 8);
 }
 
-__global__ void __launch_bounds__(512) rs16_encode_kernel(Rs16EncArgs a) {  // grid.y = segments
+#ifndef TEC_RS16_WPE
+#define TEC_RS16_WPE 6  // waves per SIMD the encode is compiled for: 6 -> 3.94 ms, 5 -> 4.75, 8 (spills) -> 4.19
+#endif
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(TEC_RS16_WPE))) rs16_encode_kernel(Rs16EncArgs a) {  // grid.y = segments
     extern __shared__ __attribute__((aligned(16))) uint16_t lds16[];
     uint16_t *lut = lds16;                     // span x 64 entries
     uint16_t *work = lds16 + a.span * 64u;     // work_len x blockDim
@@ -121,7 +124,7 @@ __global__ void __launch_bounds__(512) rs16_encode_kernel(Rs16EncArgs a) {  // g
     a.out += (uint64_t)blockIdx.y * a.seg_out;
     const Col c{work + threadIdx.x, blockDim.x};
     const uint32_t k = a.k, m = a.m, cs = a.c;
-    for (uint32_t i = 0; i < a.work_len; i++) c.st(i, 0);
+    for (uint32_t i = 0; i < (a.one_chunk ? cs : a.work_len); i++) c.st(i, 0);
     if (a.high) {
         // chunks of c originals: the first at work[0..c), each further one at work[c..2c),
         // transformed at its own skew offset and XOR-folded into the first
@@ -134,6 +137,28 @@ __global__ void __launch_bounds__(512) rs16_encode_kernel(Rs16EncArgs a) {  // g
                 for (uint32_t j = 0; j < cs; j++) c.st(j, c.ld(j) ^ c.ld(cs + j));
         }
         fft(c, lut, 0, cs, m, 0);
+    } else if (a.one_chunk) {
+        // low rate, chunk <= 32: one chunk of work in LDS; the IFFT result is kept in registers
+        // (two elements per VGPR) and restored before each chunk's FFT, which is then written out
+        for (uint32_t j = 0; j < k; j++) c.st(j, ld_elem(a.in + (uint64_t)j * a.in_stride, e));
+        ifft(c, lut, 0, cs, k, 0);
+        uint32_t keep[16];
+#pragma unroll
+        for (uint32_t q = 0; q < 16u; q++) keep[q] = 2 * q < cs ? c.ld(2 * q) | c.ld(2 * q + 1) << 16 : 0u;
+        for (uint32_t s = 0; s < m; s += cs) {
+            if (s) {
+#pragma unroll
+                for (uint32_t q = 0; q < 16u; q++)
+                    if (2 * q < cs) {
+                        c.st(2 * q, keep[q] & 0xffffu);
+                        c.st(2 * q + 1, keep[q] >> 16);
+                    }
+            }
+            const uint32_t n = m - s < cs ? m - s : cs;
+            fft(c, lut, 0, cs, n, s + cs);
+            for (uint32_t j = 0; j < n; j++) st_elem(a.out + (uint64_t)(s + j) * a.out_stride, e, c.ld(j));
+        }
+        return;
     } else {
         for (uint32_t j = 0; j < k; j++) c.st(j, ld_elem(a.in + (uint64_t)j * a.in_stride, e));
         ifft(c, lut, 0, cs, k, 0);
@@ -172,14 +197,18 @@ static uint32_t rs16_blocks(uint64_t elems) { return (uint32_t)((elems + 127) / 
 // Block size of the encode: the nibble tables (span x 128 B) are staged once per block and every
 // thread keeps work_len u16 in LDS, so larger blocks amortise the tables; pick the size that
 // keeps the most waves per CU within its 160 KB of LDS (128 threads, 32.5 KB, for OuterCoder(17,
-// 50) left 8 waves per CU; 512 threads, 80.5 KB, leave 16).
+// 50) left 8 waves per CU; 512 threads, 80.5 KB, leave 16; with one chunk of work per thread,
+// 1024 threads, 80.5 KB, leave 32).
 static uint32_t rs16_enc_threads(const Rs16EncArgs &a, size_t *lds_out) {
     uint32_t best_t = 128, best_w = 0;
     size_t best_lds = 0;
-    for (uint32_t t = 128; t <= 512; t *= 2) {
-        const size_t lds = (size_t)a.span * 128u + (size_t)a.work_len * t * 2u;
+    const uint32_t per = a.one_chunk ? a.c : a.work_len;  // u16 of work per thread
+    for (uint32_t t = 128; t <= 1024; t *= 2) {
+        const size_t lds = (size_t)a.span * 128u + (size_t)per * t * 2u;
         if (lds > 160 * 1024) break;
-        const uint32_t blocks = (uint32_t)((160 * 1024) / lds), waves = std::min(blocks * (t / 64u), 32u);
+        // whole blocks fit within the LDS and within the waves per SIMD the kernel's registers allow
+        const uint32_t blocks = std::min((uint32_t)((160 * 1024) / lds), 4u * TEC_RS16_WPE / (t / 64u));
+        const uint32_t waves = blocks * (t / 64u);
         if (waves > best_w) { best_w = waves; best_t = t; best_lds = lds; }
     }
     *lds_out = best_lds;
