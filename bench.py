@@ -221,15 +221,17 @@ def main():
         def step():
             merkle.commit_batch(d_out, per, g.slice_len, N, nobj, d_leaf, d_root, d_proof, T.SLICE_TREE_HEIGHT, stream)
 
+    if args.mode in ("decode", "recover") and args.decode_jit == "off":
+        slicer.coder.set_decode_jit("off")
+    # (recover: 20 patterns x ~64 stripes per window -- below the engine's 512-stripe floor for a
+    # pattern kernel's own launch, so it runs the shared table-driven launch either way)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     jit = None
     if args.mode in ("decode", "recover"):
-        # hot patterns' kernels compile on worker threads from the first decode on (one per
-        # stripe rotation here); wait for them, then warm up again: one-time work, untimed
-        if args.decode_jit == "off":
-            slicer.coder.set_decode_jit("off")
+        # hot patterns' kernels compile on worker threads from the first decode on; wait for
+        # them, then warm up again: one-time work, untimed
         t_jit = time.perf_counter()
         ready, pending, failed = slicer.coder.decode_jit_status()
         while pending:
@@ -380,23 +382,6 @@ def outer_bench(args, torch, dist, world, rank, dev):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    jit = None
-    if args.mode in ("decode", "recover"):
-        # hot patterns' kernels compile on worker threads from the first decode on (one per
-        # stripe rotation here); wait for them, then warm up again: one-time work, untimed
-        if args.decode_jit == "off":
-            slicer.coder.set_decode_jit("off")
-        t_jit = time.perf_counter()
-        ready, pending, failed = slicer.coder.decode_jit_status()
-        while pending:
-            ready, pending, failed = slicer.coder.decode_jit_status(timeout_ms=30_000)
-            print(f"[bench] pattern kernels: {ready} ready, {pending} compiling, {failed} failed "
-                  f"({time.perf_counter() - t_jit:.0f} s)", file=sys.stderr, flush=True)
-        jit = {"mode": args.decode_jit, "ready": ready, "failed": failed,
-               "compile_wait_s": round(time.perf_counter() - t_jit, 1)}
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     batch.kernel_time_ms()

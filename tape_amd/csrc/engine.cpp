@@ -892,6 +892,9 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     // patterns with a per-pattern kernel built (dec_rtc.cpp) leave their group for a launch of
     // their own; every staged stripe counts toward building its pattern's kernel
     struct Fixed { uint64_t key; const DecJitKernel *k; std::vector<GpeJob> jobs; size_t off = 0; };
+    constexpr uint64_t kJitMinStripes = 512;  // two workgroups per CU
+    // a caller that lowered the build threshold (te_clay_set_decode_jit, tests) lowers the floor too
+    const uint64_t jit_floor = c->jit_mode >= 0 ? std::min<uint64_t>(kJitMinStripes, c->jit_min) : kJitMinStripes;
     std::vector<Fixed> fixed;
     if (staged) {
         if (!c->jit) {
@@ -908,7 +911,11 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
             for (size_t p = 0; p < pats.size(); p++) {
                 if (!cnt[p]) continue;
                 const DecJitKernel *k = dec_jit_get(c->jit, h, cached[p]->P, cached[p]->orient, (int)geo.G, (int)geo.wb, cnt[p]);
-                if (!k) continue;
+                // a pattern kernel gets a launch of its own: only worth it for a group that fills
+                // the GPU; smaller groups stay in the shared table-driven launch (recover's
+                // windows hold ~64 stripes per pattern: 80 small launches per step ran 29.3 ms
+                // against 14.5 for the shared one)
+                if (!k || cnt[p] < jit_floor) continue;
                 fx[p] = (int)fixed.size();
                 fixed.push_back(Fixed{kv.first, k, {}});
             }
