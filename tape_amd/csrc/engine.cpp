@@ -2171,4 +2171,62 @@ int te_outer_decode(uint32_t k, uint32_t n, const uint8_t *const *chunks, size_t
     return r;
 }
 
+int te_outer_decode_device(uint32_t k, uint32_t n, const uint8_t *const *d_chunks, uint64_t chunk_bytes,
+                           uint8_t *d_out, void *stream) {
+    if (k == 0 || k > n || !d_chunks || !d_out) return TE_ERR_INVALID_ARG;
+    std::vector<uint32_t> have;
+    for (uint32_t i = 0; i < n; i++)
+        if (d_chunks[i]) have.push_back(i);
+    if (have.size() < k) return TE_ERR_NOT_ENOUGH_SLICES;   // outer.rs:127-129
+    const uint32_t m = n - k;
+    std::vector<uint32_t> miss;
+    for (uint32_t i = 0; i < k; i++)
+        if (!d_chunks[i]) miss.push_back(i);
+    if (!miss.empty() && m == 0) return TE_ERR_INVALID_LAYOUT;  // outer.rs:143-152
+    if (chunk_bytes == 0 || chunk_bytes % 64 || chunk_bytes / 2 > 0xffffffffull) return TE_ERR_INVALID_LAYOUT;
+    if (!miss.empty() && (rs16::use_high_rate(k, m) < 0 || k > kRs16MaxK)) return TE_ERR_UNSUPPORTED;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    hipStream_t s = (hipStream_t)stream;
+    int r = TE_OK;
+    for (uint32_t i = 0; i < k && r == TE_OK; i++)
+        if (d_chunks[i]) r = hip_status(hipMemcpyAsync(d_out + (size_t)i * chunk_bytes, d_chunks[i], chunk_bytes, hipMemcpyDeviceToDevice, s));
+    if (r != TE_OK || miss.empty()) return r ? r : hip_status(hipStreamSynchronize(s));
+    std::vector<uint32_t> recv(have.begin(), have.begin() + k);  // any k shards determine the originals
+    std::vector<uint16_t> D;
+    if (!rs16::decode_matrix(k, m, recv, D)) return TE_ERR_INVALID_LAYOUT;
+    const rs16::Tables &T = rs16::tables();
+    const uint32_t nm = (uint32_t)miss.size();
+    std::vector<uint16_t> lut((size_t)nm * k * 64, 0);
+    for (uint32_t i = 0; i < nm; i++)
+        for (uint32_t q = 0; q < k; q++) {
+            const uint16_t coef = D[(size_t)miss[i] * k + q];
+            if (!coef) continue;
+            for (int w = 0; w < 4; w++)
+                for (uint32_t nb = 0; nb < 16; nb++)
+                    lut[((size_t)i * k + q) * 64 + w * 16 + nb] = T.gmul((uint16_t)(nb << (4 * w)), coef);
+        }
+    // device image: pointer arrays (received, restored), then the tables
+    std::vector<const uint8_t *> ptrs;
+    for (uint32_t j = 0; j < k; j++) ptrs.push_back(d_chunks[recv[j]]);
+    for (uint32_t i = 0; i < nm; i++) ptrs.push_back(d_out + (size_t)miss[i] * chunk_bytes);
+    const size_t lut_at = ptrs.size() * sizeof(void *);
+    uint8_t *d = nullptr;
+    TE_HIP(hipMallocAsync((void **)&d, lut_at + lut.size() * sizeof(uint16_t), s));
+    r = hip_status(hipMemcpyAsync(d, ptrs.data(), lut_at, hipMemcpyHostToDevice, s));
+    if (r == TE_OK) r = hip_status(hipMemcpyAsync(d + lut_at, lut.data(), lut.size() * sizeof(uint16_t), hipMemcpyHostToDevice, s));
+    if (r == TE_OK) {
+        Rs16DecArgs a{};
+        a.recv = reinterpret_cast<const uint8_t *const *>(d);
+        a.out = reinterpret_cast<uint8_t *const *>(d + (size_t)k * sizeof(void *));
+        a.lut = reinterpret_cast<const uint16_t *>(d + lut_at);
+        a.k = k; a.nmiss = nm; a.elems = (uint32_t)(chunk_bytes / 2);
+        KTimer kt(s);
+        r = hip_status(launch_rs16_decode(a, s));
+        kt.stop();
+    }
+    const int r2 = hip_status(hipFreeAsync(d, s));
+    const int r3 = hip_status(hipStreamSynchronize(s));  // the host tables must outlive the copies
+    return r ? r : (r2 ? r2 : r3);
+}
+
 }  // extern "C"

@@ -170,8 +170,11 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(TEC_R
 }
 
 // Restore the missing originals: out[i] = sum_r D[i][r] * received[r] (nibble tables per
-// coefficient, staged in LDS).
-__global__ void __launch_bounds__(128) rs16_decode_kernel(Rs16DecArgs a) {
+// coefficient, staged in LDS).  REG (k <= 32): a thread loads its element of each received shard
+// once into registers and computes every missing output from them (the first kernel re-read the
+// k received elements for each of the nmiss outputs).
+template <bool REG>
+__global__ void __launch_bounds__(512) rs16_decode_kernel(Rs16DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lds16[];
     const uint32_t ntab = a.nmiss * a.k;
     const bool in_lds = ntab * 128u <= kRs16DecLds;  // else the tables are read from L2
@@ -183,16 +186,36 @@ __global__ void __launch_bounds__(128) rs16_decode_kernel(Rs16DecArgs a) {
     const uint16_t *tab = in_lds ? lds16 : a.lut;
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= a.elems) return;
-    for (uint32_t i = 0; i < a.nmiss; i++) {
-        uint32_t acc = 0;
-        for (uint32_t r = 0; r < a.k; r++) acc ^= mulx(ld_elem(a.recv[r], e), tab + (i * a.k + r) * 64u);
-        st_elem(a.out[i], e, acc);
+    if constexpr (REG) {
+        uint32_t x[16];  // received elements, two per register
+#pragma unroll
+        for (uint32_t q = 0; q < 16u; q++)
+            x[q] = (2 * q < a.k ? ld_elem(a.recv[2 * q], e) : 0u) | (2 * q + 1 < a.k ? ld_elem(a.recv[2 * q + 1], e) << 16 : 0u);
+#pragma unroll 1
+        for (uint32_t i = 0; i < a.nmiss; i++) {
+            const uint16_t *t = tab + i * a.k * 64u;
+            uint32_t acc = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 16u; q++) asm volatile("" : "+v"(x[q]));  // keep the nibble
+            // indices inside the loop (hoisted, 128 of them spilled)
+#pragma unroll
+            for (uint32_t q = 0; q < 16u; q++) {
+                if (2 * q < a.k) acc ^= mulx(x[q] & 0xffffu, t + 2 * q * 64u);
+                if (2 * q + 1 < a.k) acc ^= mulx(x[q] >> 16, t + (2 * q + 1) * 64u);
+            }
+            st_elem(a.out[i], e, acc);
+        }
+    } else {
+        for (uint32_t i = 0; i < a.nmiss; i++) {
+            uint32_t acc = 0;
+            for (uint32_t r = 0; r < a.k; r++) acc ^= mulx(ld_elem(a.recv[r], e), tab + (i * a.k + r) * 64u);
+            st_elem(a.out[i], e, acc);
+        }
     }
 }
 
 }  // namespace rs16k
 
-static uint32_t rs16_blocks(uint64_t elems) { return (uint32_t)((elems + 127) / 128); }
 
 // Block size of the encode: the nibble tables (span x 128 B) are staged once per block and every
 // thread keeps work_len u16 in LDS, so larger blocks amortise the tables; pick the size that
@@ -235,7 +258,10 @@ hipError_t launch_rs16_decode(const Rs16DecArgs &a, hipStream_t s) {
     if (a.elems == 0 || a.nmiss == 0) return hipSuccess;
     const size_t tab = (size_t)a.nmiss * a.k * 128u, lds = tab <= rs16k::kRs16DecLds ? tab : 0;
     if (a.k > kRs16MaxK || a.nmiss > kRs16MaxK) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(rs16k::rs16_decode_kernel, dim3(rs16_blocks(a.elems)), dim3(128), lds, s, a);
+    // 512-thread blocks: the tables (<= 48 KB) are staged once per 8 waves, not per 2
+    const dim3 grid((uint32_t)((a.elems + 511) / 512)), block(512);
+    if (a.k <= 32) hipLaunchKernelGGL(rs16k::rs16_decode_kernel<true>, grid, block, lds, s, a);
+    else hipLaunchKernelGGL(rs16k::rs16_decode_kernel<false>, grid, block, lds, s, a);
     return hipGetLastError();
 }
 

@@ -86,4 +86,16 @@ def encode_device(k: int, m: int, d_in, chunk_bytes: int, segments: int, seg_in:
     _check(r, "encode")
 
 
-__all__ = ["OuterCoder", "ReedSolomonCoder", "encode_device", "MAX_CHUNK_BYTES", "EncodeError", "DecodeError", "_lib"]
+def decode_device(k: int, n: int, chunks: list, chunk_bytes: int, d_out, stream=None) -> None:
+    """te_outer_decode_device: the k data chunks into d_out (a torch tensor of k * chunk_bytes)
+    from device chunks (`chunks[i]`: a device address, a torch tensor, or None when missing)."""
+    ptrs = (C.c_void_p * n)(*[None if c is None else (c.data_ptr() if hasattr(c, "data_ptr") else int(c))
+                              for c in chunks])
+    sp = stream.cuda_stream if stream is not None else None
+    r = lib.te_outer_decode_device(k, n, C.cast(ptrs, C.POINTER(C.c_void_p)), chunk_bytes,
+                                   C.c_void_p(d_out.data_ptr()), C.c_void_p(sp) if sp else None)
+    _check(r, "decode")
+
+
+__all__ = ["OuterCoder", "ReedSolomonCoder", "encode_device", "decode_device", "MAX_CHUNK_BYTES", "EncodeError",
+           "DecodeError", "_lib"]

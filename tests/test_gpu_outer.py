@@ -113,3 +113,27 @@ def test_rs_coder_reference_tests():
     assert len(e) == 20 and not any(c.decode(e[10:]))
     with pytest.raises(T.EncodeError):
         c.encode(bytes(10 * 4096 + 1))                                       # past MAX_SLICE_BYTES
+
+
+@pytest.mark.parametrize("k,n", [(17, 50), (40, 49), (4, 6)])
+@pytest.mark.parametrize("present", ["parity_only", "mixed", "data_only"])
+def test_decode_device_matches_original(k, n, present):
+    """te_outer_decode_device (snapshot reads on device buffers) restores the data chunks from
+    device chunks: parity-only, mixed and data-only sets, against the original bytes."""
+    import torch
+    from tape_amd import outer
+    data = np.random.default_rng(k * 100 + n).bytes(k * 64 * 1000 - 7)
+    chunks = OuterCoder(k, n).encode(data)
+    cb = len(chunks[0])
+    m = n - k
+    if present == "parity_only":
+        keep = list(range(k, k + min(k, m)))
+        keep += [i for i in range(k) if len(keep) < k][: k - len(keep)]
+    elif present == "mixed":
+        keep = sorted(random.Random(k + n).sample(range(n), k))
+    else:
+        keep = list(range(k))
+    dev = [torch.tensor(np.frombuffer(c, np.uint8), device="cuda") if i in keep else None for i, c in enumerate(chunks)]
+    d_out = torch.empty(k * cb, dtype=torch.uint8, device="cuda")
+    outer.decode_device(k, n, dev, cb, d_out)
+    assert d_out.cpu().numpy().tobytes() == b"".join(chunks[:k])
