@@ -122,7 +122,8 @@ def main():
     ap.add_argument("--mode", choices=["encode", "repair", "decode", "commit", "recover", "outer"], default="encode")
     ap.add_argument("--segments", type=int, default=16,
                     help="--mode outer: snapshot segments per step (OuterCoder(17, 50), 4 MiB chunks)")
-    ap.add_argument("--cpu-sample", type=int, default=96, help="objects in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=512,
+                    help="objects in the CPU-baseline sample (0 = skip); 512 x 4 MiB is ~12 s of CPU work on 16 threads")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = min(16, affinity cores): the GPU box grants 16 host cores per GPU (pool rules)")
     ap.add_argument("--copy-objects", type=int, default=-1,
