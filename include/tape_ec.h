@@ -237,7 +237,7 @@ int te_encode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *
 /* Batched Slicer::encode HOST -> HOST: the shape of the sdk stream writer's encode stage
  * (sdk/src/stream/write.rs:332-362: object bytes in, n slices per object out).  Offsets in
  * `objs` are relative to h_data / h_out.  Objects are pipelined through the device in windows
- * of at most `window_bytes` (input + output; 0 = 1 GiB) over three streams, so the H2D copy of
+ * of at most `window_bytes` (input + output; 0 = 128 MiB) over three streams, so the H2D copy of
  * one window, the kernels of the next and the D2H copy of a third overlap.  h_data/h_out
  * should be pinned (hipHostMalloc / hipHostRegister) for full PCIe rate.  Synchronous. */
 int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data,
@@ -253,7 +253,8 @@ int te_encode_batch_host_multi(te_clay *const *coders, size_t ncoders, const te_
  * 332-362): per object o, leaf hashes hash_leaf(slice i) at h_leaf_hashes + (o*n + i)*32, the
  * root root_from_leaf_hashes::<height> at h_roots + o*32 and, if h_proofs is not NULL, proof i
  * (create_proof_from_leaf_hashes::<height>) at h_proofs + ((o*n + i)*height + level)*32.
- * Hashed on the device from each window's slices before they are copied out.  Requires
+ * Hashed on the device from each window's slices before they are copied out (window_bytes 0 =
+ * 1 GiB: the hashing needs many slice streams per launch).  Requires
  * n <= 2^height, height <= 32 and slice_len % 4 == 0 (every Clay profile with even alpha).
  * Synchronous; objects keep their order. */
 int te_encode_commit_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data,
