@@ -260,10 +260,7 @@ struct te_clay {
     hipStream_t rec_stream = nullptr;
     // te_encode_batch_host pipeline: kPipe slots, each with its own stream, descriptor arena
     // and device window buffers, so window w+1's H2D overlaps window w's kernel and D2H.
-#ifndef TEC_PIPE
-#define TEC_PIPE 3
-#endif
-    static constexpr int kPipe = TEC_PIPE;
+    static constexpr int kPipe = 3;  // a fourth slot measured slower
     // Compiled decode patterns (layered pattern + staged plane program), by padded erasure mask:
     // building them is host work per distinct pattern (matrix inversion, program, colouring).
     struct DecCache {
