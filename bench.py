@@ -525,8 +525,8 @@ def copy_inclusive_commit(args, torch, dist, world, slicer, batch, d_in, d_out, 
     """Copy-inclusive encode + commitments (SURVEY 8f-4): BlobEncoder::encode_with_proofs per object
     (sdk/src/codec/encoder.rs:220-260) as the stream writer runs it (sdk/src/stream/write.rs:
     332-362), through te_encode_commit_batch_host: pinned object bytes in; slices, leaf hashes,
-    roots and proofs out.  Per window size: the leaf kernel's parallelism is one lane per slice,
-    so larger windows hash more slices at once."""
+    roots and proofs out.  Per group size (window_bytes: the slices a leaf launch hashes at once,
+    whose time is one slice's SHA-256 whatever the group size)."""
     m = copy_share(args, world)
     N, H = 20, 5
     h_in = torch.empty(m * L, dtype=torch.uint8).pin_memory()
@@ -537,7 +537,7 @@ def copy_inclusive_commit(args, torch, dist, world, slicer, batch, d_in, d_out, 
     proof = torch.empty(m * N * H * 32, dtype=torch.uint8).pin_memory()
     objs = batch.encode_descs([(i * L, L, i * per, 0) for i in range(m)])
     res = {}
-    for wgib in (1, 4):
+    for wgib in (2, 4):
         wb = wgib << 30
         batch.encode_commit_batch_host(slicer, h_in, objs, h_out, leaf, root, proof, window_bytes=wb)  # warm-up
         if world > 1:

@@ -253,8 +253,10 @@ int te_encode_batch_host_multi(te_clay *const *coders, size_t ncoders, const te_
  * 332-362): per object o, leaf hashes hash_leaf(slice i) at h_leaf_hashes + (o*n + i)*32, the
  * root root_from_leaf_hashes::<height> at h_roots + o*32 and, if h_proofs is not NULL, proof i
  * (create_proof_from_leaf_hashes::<height>) at h_proofs + ((o*n + i)*height + level)*32.
- * Hashed on the device from each window's slices before they are copied out (window_bytes 0 =
- * 1 GiB: the hashing needs many slice streams per launch).  Requires
+ * Hashed on the device from the slices in HBM while they are copied out: objects go through the
+ * device in groups of at most `window_bytes` (input + output; 0 = 4 GiB; three groups resident),
+ * each copied in windows of <= 128 MiB, and one leaf launch hashes a whole group (its time is
+ * one slice's SHA-256 whatever the group size, so groups are large).  Requires
  * n <= 2^height, height <= 32 and slice_len % 4 == 0 (every Clay profile with even alpha).
  * Synchronous; objects keep their order. */
 int te_encode_commit_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data,

@@ -250,6 +250,7 @@ struct te_clay {
     std::mutex mu;
     int device = 0;                // every allocation and launch of this handle runs on it
     hipStream_t stream = nullptr;  // for the synchronous host-buffer entry points
+    hipStream_t hash_stream = nullptr;  // te_encode_commit_batch_host: group hashing
     Arena enc, dec, rep, rec;
     DevBuf io_in, io_out;          // staging for host-buffer entry points
     // te_recover_batch_device workspaces (decoded objects, re-encoded slices); `rec_done` is
@@ -308,6 +309,9 @@ static void release_device_state(te_clay *c) {
     c->rec_pending = false;
     if (c->stream) (void)hipStreamDestroy(c->stream);
     c->stream = nullptr;
+    if (c->hash_stream) (void)hipStreamSynchronize(c->hash_stream);
+    if (c->hash_stream) (void)hipStreamDestroy(c->hash_stream);
+    c->hash_stream = nullptr;
     for (auto &sl : c->pipe) {
         sl.arena.release();
         sl.in.release();
@@ -1214,45 +1218,68 @@ struct CommitOut {
     uint32_t height;
 };
 
-static int encode_host_impl(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data, const te_object *objs,
-                            size_t nobj, uint8_t *h_out, size_t window_bytes, const CommitOut *co) {
-    if (!c || !cfg || (!objs && nobj) || (nobj && (!h_data || !h_out))) return TE_ERR_INVALID_ARG;
-    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
-    // default window: plain encode 128 MiB (1024 x 4 MiB pinned: 14.1 GiB/s against 12.6 at 1 GiB --
-    // smaller windows overlap the H2D, kernels and D2H more finely; 64 MiB varied 11.1-14.3, below
-    // that the per-window launches cost more; a fourth slot measured slower); with commitments
-    // 1 GiB (the leaf kernel needs many slice streams per launch)
-    if (window_bytes == 0) window_bytes = co ? (size_t)1 << 30 : (size_t)128 << 20;
-    const uint32_t n = (uint32_t)c->h.n;
-    std::vector<uint64_t> out_bytes(nobj), slice_len(nobj);
-    for (size_t i = 0; i < nobj; i++) {
-        te_geometry g;
-        te_slicer_geometry(c, objs[i].blob_len, &g);
-        slice_len[i] = g.slice_len;
-        out_bytes[i] = (uint64_t)n * g.slice_len;
-        if (co && g.slice_len % 4) return TE_ERR_INVALID_ARG;  // the leaf kernel reads dwords
-    }
-    // per-object commitment bytes (device layout within a window: leaves, then roots, then proofs)
-    const uint64_t leaf_b = (uint64_t)n * TE_HASH_SIZE, proof_b = co && co->proof ? leaf_b * co->height : 0;
+// Host <-> device copy runs of a window: consecutive objects contiguous on the host move with one DMA.
+struct CopyRun { uint64_t host, dev, len; };
 
-    std::lock_guard<std::mutex> lk(c->mu);
-    DeviceGuard dg(c->device);
-    TE_HIP(dg.err);
-    for (auto &sl : c->pipe)
-        if (!sl.s) TE_HIP(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
-    // Copy runs: consecutive objects contiguous on the host are moved with one DMA.
-    struct Run { uint64_t host, dev, len; };
-    auto add_run = [](std::vector<Run> &v, uint64_t host, uint64_t dev, uint64_t len) {
+// Device layout of objects [a, b) placed from offsets (din, dout) of a slot's buffers: the encode
+// descriptors (`local`, offsets relative to the buffers) and the H2D / D2H copy runs.
+static void window_layout(const te_object *objs, const std::vector<uint64_t> &out_bytes, size_t a, size_t b,
+                          uint64_t din, uint64_t dout, std::vector<te_object> &local, std::vector<CopyRun> &hin,
+                          std::vector<CopyRun> &hout) {
+    auto add_run = [](std::vector<CopyRun> &v, uint64_t host, uint64_t dev, uint64_t len) {
         if (!len) return;
         if (!v.empty() && v.back().host + v.back().len == host && v.back().dev + v.back().len == dev)
             v.back().len += len;
         else
             v.push_back({host, dev, len});
     };
+    local.clear();
+    hin.clear();
+    hout.clear();
+    for (size_t o = a; o < b; o++) {
+        local.push_back(te_object{din, objs[o].blob_len, dout, objs[o].chunk_index});
+        add_run(hin, objs[o].data_off, din, objs[o].blob_len);
+        add_run(hout, objs[o].out_off, dout, out_bytes[o]);
+        din += (objs[o].blob_len + 15) & ~15ull;  // device copies 16-byte aligned
+        dout += out_bytes[o];
+    }
+}
+
+static int copy_runs(const std::vector<CopyRun> &runs, uint8_t *dev, const uint8_t *host, hipMemcpyKind kind,
+                     hipStream_t s) {
+    for (const CopyRun &r : runs) {
+        const bool h2d = kind == hipMemcpyHostToDevice;
+        void *dst = h2d ? (void *)(dev + r.dev) : (void *)(host + r.host);
+        const void *src = h2d ? (const void *)(host + r.host) : (const void *)(dev + r.dev);
+        TE_HIP(hipMemcpyAsync(dst, src, r.len, kind, s));
+    }
+    return TE_OK;
+}
+
+static int encode_host_impl(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data, const te_object *objs,
+                            size_t nobj, uint8_t *h_out, size_t window_bytes) {
+    if (!c || !cfg || (!objs && nobj) || (nobj && (!h_data || !h_out))) return TE_ERR_INVALID_ARG;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    // default window 128 MiB (1024 x 4 MiB pinned: 14.1 GiB/s against 12.6 at 1 GiB -- smaller
+    // windows overlap the H2D, kernels and D2H more finely; 64 MiB varied 11.1-14.3, below that the
+    // per-window launches cost more; a fourth slot measured slower)
+    if (window_bytes == 0) window_bytes = (size_t)128 << 20;
+    const uint32_t n = (uint32_t)c->h.n;
+    std::vector<uint64_t> out_bytes(nobj);
+    for (size_t i = 0; i < nobj; i++) {
+        te_geometry g;
+        te_slicer_geometry(c, objs[i].blob_len, &g);
+        out_bytes[i] = (uint64_t)n * g.slice_len;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    TE_HIP(dg.err);
+    for (auto &sl : c->pipe)
+        if (!sl.s) TE_HIP(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
     int rc = TE_OK;
     size_t i = 0, w = 0;
     std::vector<te_object> local;
-    std::vector<Run> hin, hout;
+    std::vector<CopyRun> hin, hout;
     while (i < nobj && rc == TE_OK) {
         // window [i, j): at least one object, in + out bytes within window_bytes
         size_t j = i;
@@ -1264,60 +1291,12 @@ static int encode_host_impl(te_clay *c, const te_slicer_cfg *cfg, const uint8_t 
         }
         te_clay::Slot &sl = c->pipe[w % te_clay::kPipe];
         if ((rc = hip_status(sl.in.ensure(in_sz + 16))) || (rc = hip_status(sl.out.ensure(out_sz)))) break;
-        local.clear();
-        hin.clear();
-        hout.clear();
-        uint64_t din = 0, dout = 0;
-        for (size_t o = i; o < j; o++) {
-            local.push_back(te_object{din, objs[o].blob_len, dout, objs[o].chunk_index});
-            add_run(hin, objs[o].data_off, din, objs[o].blob_len);
-            add_run(hout, objs[o].out_off, dout, out_bytes[o]);
-            din += (objs[o].blob_len + 15) & ~15ull;
-            dout += out_bytes[o];
-        }
-        for (const Run &r : hin)
-            if ((rc = hip_status(hipMemcpyAsync(sl.in.as<uint8_t>() + r.dev, h_data + r.host, r.len,
-                                                hipMemcpyHostToDevice, sl.s))))
-                break;
-        if (rc) break;
+        window_layout(objs, out_bytes, i, j, 0, 0, local, hin, hout);
+        if ((rc = copy_runs(hin, sl.in.as<uint8_t>(), h_data, hipMemcpyHostToDevice, sl.s))) break;
         rc = encode_enqueue(c, cfg, sl.in.as<uint8_t>(), local.data(), local.size(), sl.out.as<uint8_t>(), sl.s,
                             false, &sl.arena);
         if (rc) break;
-        if (co) {  // commitments of the window's objects, one launch per run of equal slice lengths
-            const uint64_t cnt = j - i;
-            const uint64_t root_at = cnt * leaf_b, proof_at = root_at + cnt * TE_HASH_SIZE;
-            if ((rc = hip_status(sl.commit.ensure(proof_at + cnt * proof_b)))) break;
-            uint8_t *dc = sl.commit.as<uint8_t>();
-            for (size_t o = i; o < j && rc == TE_OK;) {
-                size_t e = o + 1;
-                while (e < j && slice_len[e] == slice_len[o]) e++;
-                CommitArgs a{};
-                a.slices = sl.out.as<uint8_t>() + local[o - i].out_off;
-                a.obj_stride = out_bytes[o];
-                a.slice_len = slice_len[o];
-                a.n = n;
-                a.nobj = (uint32_t)(e - o);
-                a.height = co->height;
-                a.leaf = dc + (o - i) * leaf_b;
-                a.root = dc + root_at + (o - i) * TE_HASH_SIZE;
-                a.proof = co->proof ? dc + proof_at + (o - i) * proof_b : nullptr;
-                rc = hip_status(launch_commit(a, sl.s));
-                o = e;
-            }
-            if (rc) break;
-            const struct { uint8_t *h; uint64_t d, len; } back[3] = {
-                {co->leaf + i * leaf_b, 0, cnt * leaf_b},
-                {co->root + i * TE_HASH_SIZE, root_at, cnt * TE_HASH_SIZE},
-                {co->proof ? co->proof + i * proof_b : nullptr, proof_at, cnt * proof_b}};
-            for (const auto &bk : back)
-                if (bk.h && bk.len && (rc = hip_status(hipMemcpyAsync(bk.h, dc + bk.d, bk.len, hipMemcpyDeviceToHost, sl.s))))
-                    break;
-            if (rc) break;
-        }
-        for (const Run &r : hout)
-            if ((rc = hip_status(hipMemcpyAsync(h_out + r.host, sl.out.as<uint8_t>() + r.dev, r.len,
-                                                hipMemcpyDeviceToHost, sl.s))))
-                break;
+        if ((rc = copy_runs(hout, sl.out.as<uint8_t>(), h_out, hipMemcpyDeviceToHost, sl.s))) break;
         i = j;
         w++;
     }
@@ -1325,6 +1304,162 @@ static int encode_host_impl(te_clay *c, const te_slicer_cfg *cfg, const uint8_t 
         const int r2 = hip_status(hipStreamSynchronize(sl.s));
         if (rc == TE_OK) rc = r2;
     }
+    return rc;
+}
+
+// te_encode_commit_batch_host: encode + commitments, host -> host.  The leaf kernel's time per
+// launch is one slice stream's SHA-256 (~27-30 ms for a 715 KB slice) whatever the
+// number of objects, so hashing must not sit between a window's encode and its D2H copy (hashing
+// each window on its slot stream: 9.6-10.5 GiB/s).  Objects go through the device in GROUPS of at
+// most `window_bytes` (input + output, default 4 GiB); a group's slices stay in one of three
+// resident group buffers (c->pipe[r].out) until hashed.  Each group is encoded in copy windows of
+// <= 128 MiB that rotate over the three slot streams exactly like te_encode_batch_host (H2D of the
+// window into the slot's input buffer, encode into the group buffer, D2H of its slices: copies stay
+// in stream order behind kernels and overlap across slots).  A fourth stream hashes a whole group
+// at once (one leaf/tree launch per run of equal slice lengths, then the D2H of leaf hashes, roots
+// and proofs) after every slot stream has passed the group's last window, so only the last
+// group's hashing is exposed.  A group buffer is refilled once its hashing is done.
+static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data,
+                                   const te_object *objs, size_t nobj, uint8_t *h_out, size_t group_bytes,
+                                   const CommitOut &co) {
+    if (!c || !cfg || (!objs && nobj) || (nobj && (!h_data || !h_out))) return TE_ERR_INVALID_ARG;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    if (group_bytes == 0) group_bytes = (size_t)4 << 30;
+    const uint64_t copy_bytes = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)128 << 20, group_bytes / 8));
+    const uint32_t n = (uint32_t)c->h.n;
+    std::vector<uint64_t> out_bytes(nobj), slice_len(nobj);
+    for (size_t i = 0; i < nobj; i++) {
+        te_geometry g;
+        te_slicer_geometry(c, objs[i].blob_len, &g);
+        slice_len[i] = g.slice_len;
+        out_bytes[i] = (uint64_t)n * g.slice_len;
+        if (g.slice_len % 4) return TE_ERR_INVALID_ARG;  // the leaf kernel reads dwords
+    }
+    auto in_bytes = [&](size_t o) { return (objs[o].blob_len + 15) & ~15ull; };  // device copies 16-byte aligned
+    // plan: groups [gcut[x], gcut[x+1]) and copy windows [wcut[y], wcut[y+1]) inside them
+    // groups of about equal size (a small last group would be hashed after the previous one)
+    std::vector<size_t> gcut{0}, wcut{0};
+    uint64_t total = 0, max_win_in = 16, max_group_out = 0, max_group_obj = 0;
+    for (size_t o = 0; o < nobj; o++) total += objs[o].blob_len + out_bytes[o];
+    const uint64_t target = total / std::max<uint64_t>(1, (total + group_bytes - 1) / group_bytes);
+    for (size_t i = 0; i < nobj;) {
+        size_t j = i;
+        uint64_t gsz = 0, gout = 0;
+        while (j < nobj && (j == i || (gsz < target && gsz + objs[j].blob_len + out_bytes[j] <= group_bytes))) {
+            gsz += objs[j].blob_len + out_bytes[j];
+            gout += out_bytes[j];
+            j++;
+        }
+        for (size_t a = i; a < j;) {
+            size_t b = a;
+            uint64_t win = 0, win_in = 0;
+            while (b < j && (b == a || win + objs[b].blob_len + out_bytes[b] <= copy_bytes)) {
+                win += objs[b].blob_len + out_bytes[b];
+                win_in += in_bytes(b);
+                b++;
+            }
+            max_win_in = std::max(max_win_in, win_in + 16);
+            wcut.push_back(b);
+            a = b;
+        }
+        max_group_out = std::max(max_group_out, gout);
+        max_group_obj = std::max<uint64_t>(max_group_obj, j - i);
+        gcut.push_back(j);
+        i = j;
+    }
+    // per-object commitment bytes (device layout within a group: leaves, then roots, then proofs)
+    const uint64_t leaf_b = (uint64_t)n * TE_HASH_SIZE, proof_b = co.proof ? leaf_b * co.height : 0;
+    const uint64_t commit_cap = max_group_obj * (leaf_b + TE_HASH_SIZE + proof_b);
+
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard dg(c->device);
+    TE_HIP(dg.err);
+    constexpr int P = te_clay::kPipe;
+    for (auto &sl : c->pipe)
+        if (!sl.s) TE_HIP(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
+    if (!c->hash_stream) TE_HIP(hipStreamCreateWithFlags(&c->hash_stream, hipStreamNonBlocking));
+    const hipStream_t sh = c->hash_stream;
+    // every buffer sized up front (the pipeline never reallocates under queued work)
+    const size_t ngroups = gcut.size() - 1, nring = std::min<size_t>(P, ngroups);
+    for (int k = 0; k < P && nobj; k++) TE_HIP(c->pipe[k].in.ensure(max_win_in));
+    for (size_t r = 0; r < nring; r++) {
+        TE_HIP(c->pipe[r].out.ensure(max_group_out));
+        TE_HIP(c->pipe[r].commit.ensure(commit_cap));
+    }
+    // events: per slot stream "passed its latest window", per group buffer "hashed"; a stream wait
+    // binds to the record current when it is enqueued
+    hipEvent_t ev[2 * P] = {};
+    int rc = TE_OK;
+    for (auto &e : ev)
+        if (!rc) rc = hip_status(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    hipEvent_t *ev_slot = ev, *ev_hashed = ev + P;
+    bool slot_used[P] = {};
+    std::vector<te_object> local;
+    std::vector<CopyRun> hin, hout;
+    size_t w = 0;  // global copy-window counter (slot = w % P)
+    for (size_t gi = 0; gi < ngroups && rc == TE_OK; gi++) {
+        const size_t i = gcut[gi], j = gcut[gi + 1], r = gi % P;
+        uint8_t *gout = c->pipe[r].out.as<uint8_t>();
+        if (gi >= P)  // the buffer's previous group must be hashed (and, before that, copied out)
+            for (int k = 0; k < P && !rc; k++) rc = hip_status(hipStreamWaitEvent(c->pipe[k].s, ev_hashed[r], 0));
+        uint64_t dout = 0;
+        while (rc == TE_OK && wcut[w] < j) {
+            const size_t a = wcut[w], b = wcut[w + 1];
+            const int k = (int)(w % P);
+            te_clay::Slot &sl = c->pipe[k];
+            window_layout(objs, out_bytes, a, b, 0, dout, local, hin, hout);
+            if ((rc = copy_runs(hin, sl.in.as<uint8_t>(), h_data, hipMemcpyHostToDevice, sl.s))) break;
+            if ((rc = encode_enqueue(c, cfg, sl.in.as<uint8_t>(), local.data(), local.size(), gout, sl.s, false,
+                                     &sl.arena)))
+                break;
+            if ((rc = copy_runs(hout, gout, h_out, hipMemcpyDeviceToHost, sl.s))) break;
+            if ((rc = hip_status(hipEventRecord(ev_slot[k], sl.s)))) break;
+            slot_used[k] = true;
+            for (size_t o = a; o < b; o++) dout += out_bytes[o];
+            w++;
+        }
+        for (int k = 0; k < P && !rc; k++)
+            if (slot_used[k]) rc = hip_status(hipStreamWaitEvent(sh, ev_slot[k], 0));
+        if (rc) break;
+        // commitments of the group's objects, one launch per run of equal slice lengths
+        const uint64_t cnt = j - i, root_at = cnt * leaf_b, proof_at = root_at + cnt * TE_HASH_SIZE;
+        uint8_t *dc = c->pipe[r].commit.as<uint8_t>();
+        uint64_t off = 0;
+        for (size_t o = i; o < j && rc == TE_OK;) {
+            size_t e = o + 1;
+            while (e < j && slice_len[e] == slice_len[o]) e++;
+            CommitArgs ca{};
+            ca.slices = gout + off;
+            ca.obj_stride = out_bytes[o];
+            ca.slice_len = slice_len[o];
+            ca.n = n;
+            ca.nobj = (uint32_t)(e - o);
+            ca.height = co.height;
+            ca.leaf = dc + (o - i) * leaf_b;
+            ca.root = dc + root_at + (o - i) * TE_HASH_SIZE;
+            ca.proof = co.proof ? dc + proof_at + (o - i) * proof_b : nullptr;
+            rc = hip_status(launch_commit(ca, sh));
+            off += (e - o) * out_bytes[o];
+            o = e;
+        }
+        if (rc) break;
+        const struct { uint8_t *h; uint64_t d, len; } back[3] = {
+            {co.leaf + i * leaf_b, 0, cnt * leaf_b},
+            {co.root + i * TE_HASH_SIZE, root_at, cnt * TE_HASH_SIZE},
+            {co.proof ? co.proof + i * proof_b : nullptr, proof_at, cnt * proof_b}};
+        for (const auto &bk : back)
+            if (bk.h && bk.len && (rc = hip_status(hipMemcpyAsync(bk.h, dc + bk.d, bk.len, hipMemcpyDeviceToHost, sh))))
+                break;
+        if (!rc) rc = hip_status(hipEventRecord(ev_hashed[r], sh));
+    }
+    for (auto &sl : c->pipe) {
+        const int r2 = hip_status(hipStreamSynchronize(sl.s));
+        if (rc == TE_OK) rc = r2;
+    }
+    const int r2 = hip_status(hipStreamSynchronize(sh));
+    if (rc == TE_OK) rc = r2;
+    for (auto &e : ev)
+        if (e) (void)hipEventDestroy(e);
     return rc;
 }
 
@@ -1345,7 +1480,7 @@ int te_encode_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *
 
 int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data, const te_object *objs,
                          size_t nobj, uint8_t *h_out, size_t window_bytes) {
-    return encode_host_impl(c, cfg, h_data, objs, nobj, h_out, window_bytes, nullptr);
+    return encode_host_impl(c, cfg, h_data, objs, nobj, h_out, window_bytes);
 }
 
 int te_encode_commit_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data, const te_object *objs,
@@ -1357,7 +1492,7 @@ int te_encode_commit_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint
     if (n > TE_COMMIT_MAX_LEAVES) return TE_ERR_INVALID_ARG;
     if (height < 64 && (uint64_t)n > (1ull << height)) return TE_ERR_MERKLE_TREE_FULL;
     const CommitOut co{h_leaf_hashes, h_roots, h_proofs, height};
-    return encode_host_impl(c, cfg, h_data, objs, nobj, h_out, window_bytes, &co);
+    return encode_commit_host_impl(c, cfg, h_data, objs, nobj, h_out, window_bytes, co);
 }
 int te_encode_batch_host_multi(te_clay *const *coders, size_t ncoders, const te_slicer_cfg *cfg, const uint8_t *h_data,
                                const te_object *objs, size_t nobj, uint8_t *h_out, size_t window_bytes) {

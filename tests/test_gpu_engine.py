@@ -230,7 +230,7 @@ def test_odd_offsets_encode_decode(oracle, sizes):
     assert not dec[:3].any() and not dec[c:].any()  # nothing written outside the objects
 
 
-@pytest.mark.parametrize("window", [0, 24 * MiB])
+@pytest.mark.parametrize("window", [0, 24 * MiB, 64 * MiB])
 def test_encode_commit_batch_host(oracle, window):
     """te_encode_commit_batch_host = BlobEncoder::encode_with_proofs per object (encoder.rs:220-260)
     over a host -> host pipeline: slices equal the oracle's, leaf hashes / roots / proofs equal the
