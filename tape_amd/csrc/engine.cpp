@@ -250,7 +250,6 @@ struct te_clay {
     std::mutex mu;
     int device = 0;                // every allocation and launch of this handle runs on it
     hipStream_t stream = nullptr;  // for the synchronous host-buffer entry points
-    hipStream_t hash_stream = nullptr;  // te_encode_commit_batch_host: group hashing
     Arena enc, dec, rep, rec;
     DevBuf io_in, io_out;          // staging for host-buffer entry points
     // te_recover_batch_device workspaces (decoded objects, re-encoded slices); `rec_done` is
@@ -309,9 +308,6 @@ static void release_device_state(te_clay *c) {
     c->rec_pending = false;
     if (c->stream) (void)hipStreamDestroy(c->stream);
     c->stream = nullptr;
-    if (c->hash_stream) (void)hipStreamSynchronize(c->hash_stream);
-    if (c->hash_stream) (void)hipStreamDestroy(c->hash_stream);
-    c->hash_stream = nullptr;
     for (auto &sl : c->pipe) {
         sl.arena.release();
         sl.in.release();
@@ -1313,9 +1309,9 @@ static int encode_host_impl(te_clay *c, const te_slicer_cfg *cfg, const uint8_t 
 // each window on its slot stream: 9.6-10.5 GiB/s).  Objects go through the device in GROUPS of at
 // most `window_bytes` (input + output, default 4 GiB); a group's slices stay in one of three
 // resident group buffers (c->pipe[r].out) until hashed.  Each group is encoded in copy windows of
-// <= 128 MiB that rotate over the three slot streams exactly like te_encode_batch_host (H2D of the
+// <= 128 MiB that rotate over two slot streams like te_encode_batch_host's three (H2D of the
 // window into the slot's input buffer, encode into the group buffer, D2H of its slices: copies stay
-// in stream order behind kernels and overlap across slots).  A fourth stream hashes a whole group
+// in stream order behind kernels and overlap across slots).  The handle's stream hashes a whole group
 // at once (one leaf/tree launch per run of equal slice lengths, then the D2H of leaf hashes, roots
 // and proofs) after every slot stream has passed the group's last window, so only the last
 // group's hashing is exposed.  A group buffer is refilled once its hashing is done.
@@ -1377,11 +1373,18 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
     constexpr int P = te_clay::kPipe;
     for (auto &sl : c->pipe)
         if (!sl.s) TE_HIP(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
-    if (!c->hash_stream) TE_HIP(hipStreamCreateWithFlags(&c->hash_stream, hipStreamNonBlocking));
-    const hipStream_t sh = c->hash_stream;
+    // the hashing runs on the handle's own stream (idle here: the handle is locked), so the call
+    // uses four streams -- the process's four hardware queues; a fifth stream shared a queue with
+    // a slot stream in bench.py (9.5 against 12.1 GiB/s in a process with no other streams)
+    if (!c->stream) TE_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    const hipStream_t sh = c->stream;
+    // copy windows rotate over two slot streams: with the hashing stream and the caller's stream
+    // that is four streams for four hardware queues (three slots: 9.5 against 12.0 GiB/s on one
+    // box, 1024 x 4 MiB, in a process that had used its current stream, as bench.py has)
+    constexpr int S = 2;
     // every buffer sized up front (the pipeline never reallocates under queued work)
     const size_t ngroups = gcut.size() - 1, nring = std::min<size_t>(P, ngroups);
-    for (int k = 0; k < P && nobj; k++) TE_HIP(c->pipe[k].in.ensure(max_win_in));
+    for (int k = 0; k < S && nobj; k++) TE_HIP(c->pipe[k].in.ensure(max_win_in));
     for (size_t r = 0; r < nring; r++) {
         TE_HIP(c->pipe[r].out.ensure(max_group_out));
         TE_HIP(c->pipe[r].commit.ensure(commit_cap));
@@ -1396,16 +1399,16 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
     bool slot_used[P] = {};
     std::vector<te_object> local;
     std::vector<CopyRun> hin, hout;
-    size_t w = 0;  // global copy-window counter (slot = w % P)
+    size_t w = 0;  // global copy-window counter (slot = w % S)
     for (size_t gi = 0; gi < ngroups && rc == TE_OK; gi++) {
         const size_t i = gcut[gi], j = gcut[gi + 1], r = gi % P;
         uint8_t *gout = c->pipe[r].out.as<uint8_t>();
         if (gi >= P)  // the buffer's previous group must be hashed (and, before that, copied out)
-            for (int k = 0; k < P && !rc; k++) rc = hip_status(hipStreamWaitEvent(c->pipe[k].s, ev_hashed[r], 0));
+            for (int k = 0; k < S && !rc; k++) rc = hip_status(hipStreamWaitEvent(c->pipe[k].s, ev_hashed[r], 0));
         uint64_t dout = 0;
         while (rc == TE_OK && wcut[w] < j) {
             const size_t a = wcut[w], b = wcut[w + 1];
-            const int k = (int)(w % P);
+            const int k = (int)(w % S);
             te_clay::Slot &sl = c->pipe[k];
             window_layout(objs, out_bytes, a, b, 0, dout, local, hin, hout);
             if ((rc = copy_runs(hin, sl.in.as<uint8_t>(), h_data, hipMemcpyHostToDevice, sl.s))) break;
