@@ -1389,14 +1389,14 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
         TE_HIP(c->pipe[r].out.ensure(max_group_out));
         TE_HIP(c->pipe[r].commit.ensure(commit_cap));
     }
-    // events: per slot stream "passed its latest window", per group buffer "hashed"; a stream wait
-    // binds to the record current when it is enqueued
-    hipEvent_t ev[2 * P] = {};
+    // events: per slot stream "encoded its latest window" and "copied it out", per group buffer
+    // "hashed" (which implies copied out); a stream wait binds to the record current when enqueued
+    hipEvent_t ev[3 * P] = {};
     int rc = TE_OK;
     for (auto &e : ev)
         if (!rc) rc = hip_status(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    hipEvent_t *ev_slot = ev, *ev_hashed = ev + P;
-    bool slot_used[P] = {};
+    hipEvent_t *ev_enc = ev, *ev_slot = ev + P, *ev_hashed = ev + 2 * P;
+    bool slot_used[S] = {};
     std::vector<te_object> local;
     std::vector<CopyRun> hin, hout;
     size_t w = 0;  // global copy-window counter (slot = w % S)
@@ -1415,14 +1415,17 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
             if ((rc = encode_enqueue(c, cfg, sl.in.as<uint8_t>(), local.data(), local.size(), gout, sl.s, false,
                                      &sl.arena)))
                 break;
+            if ((rc = hip_status(hipEventRecord(ev_enc[k], sl.s)))) break;
             if ((rc = copy_runs(hout, gout, h_out, hipMemcpyDeviceToHost, sl.s))) break;
             if ((rc = hip_status(hipEventRecord(ev_slot[k], sl.s)))) break;
             slot_used[k] = true;
             for (size_t o = a; o < b; o++) dout += out_bytes[o];
             w++;
         }
-        for (int k = 0; k < P && !rc; k++)
-            if (slot_used[k]) rc = hip_status(hipStreamWaitEvent(sh, ev_slot[k], 0));
+        // hashing starts once the group is encoded, not copied out: the last windows' D2H overlaps
+        // it (11.9 -> 12.4-12.6 GiB/s, one box)
+        for (int k = 0; k < S && !rc; k++)
+            if (slot_used[k]) rc = hip_status(hipStreamWaitEvent(sh, ev_enc[k], 0));
         if (rc) break;
         // commitments of the group's objects, one launch per run of equal slice lengths
         const uint64_t cnt = j - i, root_at = cnt * leaf_b, proof_at = root_at + cnt * TE_HASH_SIZE;
@@ -1453,6 +1456,8 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
         for (const auto &bk : back)
             if (bk.h && bk.len && (rc = hip_status(hipMemcpyAsync(bk.h, dc + bk.d, bk.len, hipMemcpyDeviceToHost, sh))))
                 break;
+        for (int k = 0; k < S && !rc; k++)
+            if (slot_used[k]) rc = hip_status(hipStreamWaitEvent(sh, ev_slot[k], 0));
         if (!rc) rc = hip_status(hipEventRecord(ev_hashed[r], sh));
     }
     for (auto &sl : c->pipe) {
