@@ -10,6 +10,7 @@
 #include <string.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <deque>
 #include <map>
 #include <unordered_map>
 #include <mutex>
@@ -1405,6 +1406,12 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
         uint8_t *gout = c->pipe[r].out.as<uint8_t>();
         if (gi >= P)  // the buffer's previous group must be hashed (and, before that, copied out)
             for (int k = 0; k < S && !rc; k++) rc = hip_status(hipStreamWaitEvent(c->pipe[k].s, ev_hashed[r], 0));
+        // In the last group the encodes run ahead of the copies (one D2H per two encodes on a slot,
+        // the rest after the group's last encode), so its hashing -- the only exposed one --
+        // starts about halfway through the group's copies instead of at their end.
+        const bool last = gi + 1 == ngroups;
+        std::deque<std::vector<CopyRun>> pend[S];
+        int encs[S] = {};
         uint64_t dout = 0;
         while (rc == TE_OK && wcut[w] < j) {
             const size_t a = wcut[w], b = wcut[w + 1];
@@ -1416,12 +1423,21 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
                                      &sl.arena)))
                 break;
             if ((rc = hip_status(hipEventRecord(ev_enc[k], sl.s)))) break;
-            if ((rc = copy_runs(hout, gout, h_out, hipMemcpyDeviceToHost, sl.s))) break;
-            if ((rc = hip_status(hipEventRecord(ev_slot[k], sl.s)))) break;
+            pend[k].push_back(hout);
+            if (!last || ++encs[k] % 2 == 0) {
+                if ((rc = copy_runs(pend[k].front(), gout, h_out, hipMemcpyDeviceToHost, sl.s))) break;
+                pend[k].pop_front();
+            }
             slot_used[k] = true;
             for (size_t o = a; o < b; o++) dout += out_bytes[o];
             w++;
         }
+        for (int k = 0; k < S && !rc; k++) {
+            for (; !pend[k].empty() && !rc; pend[k].pop_front())
+                rc = copy_runs(pend[k].front(), gout, h_out, hipMemcpyDeviceToHost, c->pipe[k].s);
+            if (!rc && slot_used[k]) rc = hip_status(hipEventRecord(ev_slot[k], c->pipe[k].s));
+        }
+        if (rc) break;
         // hashing starts once the group is encoded, not copied out: the last windows' D2H overlaps
         // it (11.9 -> 12.4-12.6 GiB/s, one box)
         for (int k = 0; k < S && !rc; k++)
