@@ -256,7 +256,8 @@ int te_encode_batch_host_multi(te_clay *const *coders, size_t ncoders, const te_
  * Hashed on the device from the slices in HBM while they are copied out: objects go through the
  * device in groups of at most `window_bytes` (input + output; 0 = 4 GiB; three groups resident),
  * each copied in windows of <= 128 MiB, and one leaf launch hashes a whole group (its time is
- * one slice's SHA-256 whatever the group size, so groups are large).  Requires
+ * one slice's SHA-256 whatever the group size, so groups are large).  The handle keeps the three
+ * group buffers allocated between calls (te_clay_free frees them).  Requires
  * n <= 2^height, height <= 32 and slice_len % 4 == 0 (every Clay profile with even alpha).
  * Synchronous; objects keep their order. */
 int te_encode_commit_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data,
