@@ -32,8 +32,8 @@ ALG_BYTES = {  # algorithmic HBM bytes per 4 MiB object
     "repair": 16 * 71_500 + 715_048,
     "decode": 7 * 715_048 + 4 * MiB,
     "commit": N * 715_048 + N * 32 + 32 + N * 5 * 32,  # slices read; leaf hashes, root, proofs written
-    # decode (7 slices in, object out) + encode (object in, 20 slices out) + the lost slice copied
-    "recover": (7 * 715_048 + 4 * MiB) + (4 * MiB + N * 715_048) + 2 * 715_048,
+    # the work, not the implementation: 7 peer slices read, the lost slice written (recover.rs:411-442)
+    "recover": 7 * 715_048 + 715_048,
 }
 
 
@@ -87,7 +87,7 @@ def dist_setup(torch, dist, backend: str):
 # scripts/profile_modes.sh + scripts/traffic.py; it is used only while the names still match.
 KERNELS = {
     "encode": ["tec::dma::enc_dma_kernel<false>"],
-    "repair": ["tec::rfold::rep_fold_kernel<0, 6>", "tec::rfold::rep_fold_kernel<1, 6>"],
+    "repair": ["tec::rfold::rep_fold_kernel"],  # every folded instance (lost column x known set)
     "decode": ["tec_dec_fixed"],  # the pattern kernels (dec_rtc.cpp); --decode-jit off: dec_stage_kernel<7, 6>
     "commit": ["tec::commit::leaf_kernel", "tec::commit::tree_kernel"],
 }
@@ -133,6 +133,9 @@ def main():
     ap.add_argument("--decode-jit", choices=["async", "off"], default="async",
                     help="decode / recover: per-pattern decode kernels (hipRTC-built during warm-up) or "
                          "the table-driven kernel only")
+    ap.add_argument("--unavailable", type=int, default=0, choices=[0, 1],
+                    help="--mode repair: 1 = slice (lost + 10) mod 20 is down too, so every stripe's "
+                         "helper set skips one node of the other column (a peer outage)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -182,7 +185,8 @@ def main():
         plans, blobs, offs, cur = [], [], [], 0
         for i in range(nobj):
             lost = i % N
-            avail = [j for j in range(N) if j != lost]
+            down = (lost + 10) % N if args.unavailable else lost
+            avail = [j for j in range(N) if j not in (lost, down)]
             p = slicer.repair_plan_from_params(lost, avail, L, g.stripe_size)
             o = {}
             for h in avail:
@@ -338,7 +342,9 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (SplitMix64 per object, seed 0x7A9E5EED ^ id), device-resident",
-            "config": {"workload": {"encode": "Slicer::encode", "repair": "Slicer::repair (lost = i mod 20)",
+            "config": {"workload": {"encode": "Slicer::encode",
+                                    "repair": "Slicer::repair (lost = i mod 20" +
+                                              (", slice (i + 10) mod 20 down)" if args.unavailable else ")"),
                                     "decode": "Slicer::decode (slices 0..12 erased)",
                                     "commit": "encode_with_proofs commitment (SHA-256 leaf per slice, height-5 root, 20 proofs)",
                                     "recover": "node recover (decode from 7 slices + re-encode, lost = i mod 20)"}[args.mode]
@@ -555,8 +561,38 @@ def copy_inclusive_commit(args, torch, dist, world, slicer, batch, d_in, d_out, 
         sl = h_out[i * sl_len:(i + 1) * sl_len].numpy().tobytes()
         ok = ok and leaf[i * 32:(i + 1) * 32].numpy().tobytes() == hashlib.sha256(b"LEAF" + sl).digest()
     best = max(res.values())
+    # te_stream_writer: the same work as per-window submissions, the stream writer's
+    # shape (sdk/src/stream/write.rs:332-362): windows of `wobj` objects, at most 4 in flight (the
+    # SDK's FuturesOrdered depth), each waited for in order before the 5th is submitted
+    stream = {}
+    sw = batch.StreamWriter([slicer], height=H, group_bytes=4 << 30)
+
+    def run_stream(wobj):
+        wins = [(a, min(m, a + wobj)) for a in range(0, m, wobj)]
+        t = 0
+        for a, b in wins:
+            objs_w = batch.encode_descs([(i * L, L, i * per, 0) for i in range(a, b)])
+            t = sw.submit(h_in, objs_w, h_out, leaf[a * N * 32:], root[a * 32:], proof[a * N * H * 32:])
+            if t > 4:
+                sw.wait(t - 4)
+        sw.wait(t)
+
+    for wobj in (64, 128):
+        if wobj > m:
+            continue
+        run_stream(wobj)  # warm-up (buffers)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.copy_steps):
+            run_stream(wobj)
+        el = max_over_ranks(torch, dist, world, time.perf_counter() - t0, dev)
+        stream[f"window_{wobj}_objects_GiBps"] = round(m * world * args.copy_steps * L / el / 2**30, 3)
+    sw.close()
+    ok2 = bool(torch.equal(h_out[:per], d_out[:per].cpu()))
     return {"value": best, "unit": "GiB/s", "objects_per_gpu": m, "steps": args.copy_steps, "pinned": True,
-            "tree_height": H, "proofs": True, "by_window": res, "matches_device_resident": ok}
+            "tree_height": H, "proofs": True, "by_window": res, "matches_device_resident": ok and ok2,
+            "stream_writer": {"in_flight": 4, "group_bytes": 4 << 30, **stream}}
 
 
 def cpu_baseline(args, np, torch, d_in, d_out, per, L):

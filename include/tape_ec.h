@@ -265,6 +265,29 @@ int te_encode_commit_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint
                                 uint8_t *h_leaf_hashes, uint8_t *h_roots, uint8_t *h_proofs,
                                 size_t window_bytes);
 
+/* Ordered, asynchronous window submission: the stream writer's encode stage
+ * (sdk/src/stream/write.rs:332-362 keeps up to min(cores, 4) chunk encodes in flight and hands them
+ * on in order through FuturesOrdered) as one GPU pipeline per handle.
+ *   te_stream_writer_new: over ncoders device-bound handles (one per GPU); window t goes to handle
+ *     (t - 1) mod ncoders.  Hashing groups of at most group_bytes (input + output; 0 = 1 GiB),
+ *     three resident per handle.  The writer owns its streams and device buffers; the handles must
+ *     outlive it and must not be re-bound to another device meanwhile.
+ *   te_stream_submit: enqueue one window -- te_encode_commit_batch_host's outputs for its objects
+ *     (slices at h_out + out_off, leaf hashes, roots, proofs if h_proofs is not NULL) -- and return
+ *     its ticket (1, 2, ... in submission order) without waiting for the device: window t+1's
+ *     encode overlaps window t's hashing and copies.  Every host buffer of the window must stay
+ *     valid (pinned for full overlap) until te_stream_wait has returned for its ticket.
+ *   te_stream_wait: complete every window up to `ticket`, in submission order; returns the first
+ *     failure among the windows it completes (TE_OK if none).
+ *   te_stream_writer_free: waits for every window, then frees the writer. */
+typedef struct te_stream_writer te_stream_writer;
+int te_stream_writer_new(te_clay *const *coders, size_t ncoders, const te_slicer_cfg *cfg, uint32_t height,
+                         size_t group_bytes, te_stream_writer **out);
+int te_stream_submit(te_stream_writer *w, const uint8_t *h_data, const te_object *objs, size_t nobj, uint8_t *h_out,
+                     uint8_t *h_leaf_hashes, uint8_t *h_roots, uint8_t *h_proofs, uint64_t *ticket);
+int te_stream_wait(te_stream_writer *w, uint64_t ticket);
+void te_stream_writer_free(te_stream_writer *w);
+
 typedef struct te_decode_object {
     uint64_t slices_off;  /* slice i at d_slices + slices_off + i*slice_len */
     uint64_t slice_len;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun call: optional GPU tests, bench lines, and a rocprofv3 kernel-stats pass.
 #   TESTS="repair or recover"  pytest -m gpu -k expression ("all" = whole suite, empty = none)
-#   MODES="repair decode"  bench.py --mode lines (env BENCH_ENV is prepended, e.g. TEC_REPAIR_KERNEL=stage)
+#   MODES="repair decode"  bench.py --mode lines (env BENCH_ENV is prepended, e.g. TEC_DEBUG_KNOBS=1 TEC_REPAIR_KERNEL=stage)
 #   PROF="repair"          bench modes to run under rocprofv3 --kernel-trace --stats
 # Every GPU step has its own time limit and the script stops at the first failure.
 set -o pipefail

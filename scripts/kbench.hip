@@ -8,6 +8,11 @@
 #include <map>
 #include <algorithm>
 using namespace tec;
+namespace tec {  // the library's per-device helper (engine.cpp), single-device here
+hipError_t ensure_dyn_lds(const void *fn, size_t bytes) {
+    return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+}  // namespace tec
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 

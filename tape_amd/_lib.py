@@ -147,6 +147,10 @@ def _load() -> C.CDLL:
                                            vp, sz]),
         "te_encode_commit_batch_host": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz, vp,
                                             C.c_uint32, vp, vp, vp, sz]),
+        "te_stream_writer_new": (i, [C.POINTER(vp), sz, C.POINTER(te_slicer_cfg), C.c_uint32, sz, C.POINTER(vp)]),
+        "te_stream_submit": (i, [vp, vp, C.POINTER(te_object), sz, vp, vp, vp, vp, C.POINTER(u64)]),
+        "te_stream_wait": (i, [vp, u64]),
+        "te_stream_writer_free": (None, [vp]),
         "te_decode_batch_device": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_decode_object), u8p, sz,
                                        vp, vp]),
         "te_repair_batch_device": (i, [vp, vp, C.POINTER(te_repair_object), sz, vp, vp]),

@@ -74,6 +74,49 @@ def encode_commit_batch_host(slicer: Slicer, data, objs: list[tuple[int, int, in
     _check(r, "encode")
 
 
+class StreamWriter:
+    """te_stream_writer: the stream writer's ordered encode stage (sdk/src/stream/write.rs:332-362,
+    FuturesOrdered over chunk encodes) as one GPU pipeline per handle.  submit() enqueues a window --
+    te_encode_commit_batch_host's outputs for its objects -- and returns its ticket at once; wait()
+    completes every window up to a ticket in submission order.  The window's host buffers (pinned
+    for full overlap) are kept referenced here until its ticket has been waited for."""
+
+    def __init__(self, slicers: list[Slicer], height: int = SLICE_TREE_HEIGHT, group_bytes: int = 0):
+        self._cfg = slicers[0]._cfg()
+        self._coders = [s.coder for s in slicers]  # the handles outlive the writer
+        hs = (C.c_void_p * len(slicers))(*[s.coder.handle.value for s in slicers])
+        h = C.c_void_p()
+        _check(lib.te_stream_writer_new(hs, len(slicers), C.byref(self._cfg), height, group_bytes, C.byref(h)),
+               "encode")
+        self._h = h
+        self._keep = {}
+
+    def submit(self, data, objs, out, leaf_hashes, roots, proofs=None) -> int:
+        arr = objs if _is_desc(objs) else encode_descs(objs)
+        t = C.c_uint64()
+        pp = C.c_void_p(_host_ptr(proofs)) if proofs is not None else None
+        r = lib.te_stream_submit(self._h, C.c_void_p(_host_ptr(data)), arr, len(arr), C.c_void_p(_host_ptr(out)),
+                                 C.c_void_p(_host_ptr(leaf_hashes)), C.c_void_p(_host_ptr(roots)), pp, C.byref(t))
+        self._keep[t.value] = (data, arr, out, leaf_hashes, roots, proofs)
+        _check(r, "encode")
+        return t.value
+
+    def wait(self, ticket: int) -> None:
+        r = lib.te_stream_wait(self._h, ticket)
+        for t in [t for t in self._keep if t <= ticket]:
+            del self._keep[t]
+        _check(r, "encode")
+
+    def close(self) -> None:
+        if self._h:
+            lib.te_stream_writer_free(self._h)
+            self._h = None
+            self._keep.clear()
+
+    def __del__(self):
+        self.close()
+
+
 def kernel_timing(enable: bool) -> None:
     """te_kernel_timing: record HIP events around every batch call's kernel launches."""
     _check(lib.te_kernel_timing(1 if enable else 0), "kernel timing")

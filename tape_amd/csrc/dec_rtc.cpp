@@ -49,6 +49,8 @@ struct DecJit {
     uint64_t min_stripes = 1024;  // ~1 GB of 1 MB stripes before a pattern is compiled
     int device = 0;
     int running = 0;              // compiles in flight
+    int holders = 0;              // status readers inside dec_jit_counts (dec_jit_hold)
+    bool closing = false;         // dec_jit_free: queued compiles give up, waiters return
     std::map<uint64_t, std::unique_ptr<Entry>> ents;
     std::vector<std::thread> threads;
 };
@@ -56,10 +58,10 @@ struct DecJit {
 DecJit *dec_jit_new(int device) {
     DecJit *j = new DecJit();
     j->device = device;
-    if (const char *e = getenv("TEC_DEC_JIT")) {
+    if (const char *e = tec_knob("TEC_DEC_JIT")) {
         j->mode = !strcmp(e, "off") || !strcmp(e, "0") ? 0 : !strcmp(e, "sync") ? 2 : 1;
     }
-    if (const char *e = getenv("TEC_DEC_JIT_MIN")) j->min_stripes = strtoull(e, nullptr, 10);
+    if (const char *e = tec_knob("TEC_DEC_JIT_MIN")) j->min_stripes = strtoull(e, nullptr, 10);
     return j;
 }
 
@@ -67,7 +69,13 @@ DecJit *dec_jit_new(int device) {
 // may run them, on the handle's device.
 void dec_jit_free(DecJit *j) {
     if (!j) return;
-    for (auto &t : j->threads) t.join();
+    {
+        std::unique_lock<std::mutex> g(j->mu);
+        j->closing = true;  // queued compiles give up without compiling
+        j->cv.notify_all();
+        j->cv.wait(g, [&] { return j->holders == 0; });
+    }
+    for (auto &t : j->threads) t.join();  // at most kMaxCompiles were compiling
     for (auto &kv : j->ents)
         if (kv.second->mod) (void)hipModuleUnload(kv.second->mod);
     delete j;
@@ -79,6 +87,17 @@ void dec_jit_set(DecJit *j, int mode, uint64_t min_stripes) {
     j->min_stripes = min_stripes;
 }
 
+void dec_jit_hold(DecJit *j) {
+    std::lock_guard<std::mutex> g(j->mu);
+    j->holders++;
+}
+
+void dec_jit_unhold(DecJit *j) {
+    std::lock_guard<std::mutex> g(j->mu);
+    j->holders--;
+    j->cv.notify_all();
+}
+
 void dec_jit_counts(DecJit *j, uint32_t timeout_ms, uint32_t *ready, uint32_t *pending, uint32_t *failed) {
     std::unique_lock<std::mutex> g(j->mu);
     auto busy = [&] {
@@ -86,7 +105,8 @@ void dec_jit_counts(DecJit *j, uint32_t timeout_ms, uint32_t *ready, uint32_t *p
             if (kv.second->state.load() == 1) return true;
         return false;
     };
-    if (timeout_ms) j->cv.wait_for(g, std::chrono::milliseconds(timeout_ms), [&] { return !busy(); });
+    if (timeout_ms)
+        j->cv.wait_for(g, std::chrono::milliseconds(timeout_ms), [&] { return j->closing || !busy(); });
     uint32_t r = 0, p = 0, f = 0;
     for (auto &kv : j->ents) {
         const int s = kv.second->state.load();
@@ -102,7 +122,7 @@ DecJitGeom dec_jit_geom(uint32_t sc) {
     // same on one box (4.71-4.72 vs 4.67-4.71 ms per 1024 x 4 MiB worst-case step) and compile
     // twice as long, so 4-column lanes are the default
     static const uint32_t wb_env = [] {
-        const char *e = getenv("TEC_DEC_JIT_WB");
+        const char *e = tec_knob("TEC_DEC_JIT_WB");
         return e && !strcmp(e, "8") ? 8u : 4u;
     }();
     DecJitGeom g{};
@@ -110,7 +130,7 @@ DecJitGeom dec_jit_geom(uint32_t sc) {
     g.wps = (sc + g.wb - 1) / g.wb;
     const uint32_t groups = (g.wps + 63) / 64;
     static const uint32_t g_env = [] {  // waves per workgroup (TEC_DEC_JIT_G, measurement knob)
-        const char *e = getenv("TEC_DEC_JIT_G");
+        const char *e = tec_knob("TEC_DEC_JIT_G");
         const int v = e ? atoi(e) : 6;
         return (uint32_t)(v >= 1 && v <= 6 ? v : 6);
     }();
@@ -122,7 +142,13 @@ DecJitGeom dec_jit_geom(uint32_t sc) {
 static void compile(DecJit *j, Entry *E, std::string src, size_t lds, uint32_t nscratch, uint32_t wb, bool queued) {
     if (queued) {  // a worker: at most kMaxCompiles compile at once
         std::unique_lock<std::mutex> g(j->mu);
-        j->cv.wait(g, [&] { return j->running < kMaxCompiles; });
+        j->cv.wait(g, [&] { return j->closing || j->running < kMaxCompiles; });
+        if (j->closing) {  // the handle is being freed or re-bound
+            E->err = "cancelled";
+            E->state.store(-1);
+            j->cv.notify_all();
+            return;
+        }
         j->running++;
     }
     std::string err;
@@ -200,7 +226,7 @@ const DecJitKernel *dec_jit_get(DecJit *j, const ClayHost &h, const GpePattern &
     for (size_t e = 0; e < erased.size(); e++)
         for (size_t k = 0; k < known.size(); k++) D[e][k] = Dm.v[e][k];
     static const bool direct = [] {  // TEC_DEC_JIT_OUT=stage: rows staged in LDS, flushed whole (measurement)
-        const char *e = getenv("TEC_DEC_JIT_OUT");
+        const char *e = tec_knob("TEC_DEC_JIT_OUT");
         return !(e && !strcmp(e, "stage"));
     }();
     if (!direct) wb = 4;  // the staged form (measurement only) has 4-column lanes

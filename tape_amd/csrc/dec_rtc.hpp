@@ -16,7 +16,7 @@ constexpr const char *kDecFixedKernel = "tec_dec_fixed";
 // waves per SIMD the 8-column kernels are compiled for (TEC_DEC_JIT_WPE, measurement knob)
 inline int dec_fixed_wpe8() {
     static const int w = [] {
-        const char *e = getenv("TEC_DEC_JIT_WPE");
+        const char *e = tec_knob("TEC_DEC_JIT_WPE");
         const int v = e ? atoi(e) : 3;  // 3: 4.78 ms; 2: 5.34; 4: spills, 7.88 (1024 x 4 MiB, 13 erasures)
         return v >= 1 && v <= 8 ? v : 3;
     }();

@@ -309,13 +309,8 @@ size_t decode_stage_scratch_bytes(const DecArgs &a) {
 template <int NK, int G>
 static hipError_t launch_dec_g(const DecArgs &a, uint64_t blocks, hipStream_t s) {
     const size_t lds = (size_t)a.lds_rows * G * 256u;
-    static size_t lds_set = 0;
-    if (lds > lds_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(dstage::dec_stage_kernel<NK, G>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        lds_set = lds;
-    }
+    hipError_t e = ensure_dyn_lds(reinterpret_cast<const void *>(dstage::dec_stage_kernel<NK, G>), lds);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((dstage::dec_stage_kernel<NK, G>), dim3((uint32_t)blocks), dim3(G * 64), lds, s, a);
     return hipGetLastError();
 }

@@ -61,14 +61,16 @@ constexpr uint32_t kDrop = 0x80000000u;    // offset past every resource: the ra
 #endif
 #ifndef TEC_DMA_ORDER
 #define TEC_DMA_ORDER 1   // 1: a step's stores are issued before the next plane's DMA (B1 waits vmcnt(0));
-                          // 0: DMA first, B1 waits vmcnt(2) (measured 3 % slower)
+                          // 0: DMA first, B1 waits vmcnt(2) (measured 3 % slower);
+                          // 2: DMA first, B1 waits only for it: the previous step's stores stay in flight
 #endif
 #ifndef TEC_DMA_STORE_MASK
 #define TEC_DMA_STORE_MASK 1  // per-job chunk filter (te_recover_batch_device); 0: timing builds only
 #endif
 #ifndef TEC_DMA_ABLATE
 #define TEC_DMA_ABLATE 0  // timing builds only (scripts/kbench.hip): bit0 no stores, bit1 no DMA,
-#endif                    // bit2 trivial MDS, bit3 no vmcnt wait at B1, bit4 no B2 barrier
+#endif                    // bit2 trivial MDS, bit3 no vmcnt wait at B1, bit4 no B2 barrier,
+                          // bit6 no partner DMA, bit7 no level-2 partner DMA
 
 // Staging rows (per plane).
 constexpr int kRowC0 = 0;   // 0..2: node 7+r at this plane (level 1 parity; level 2 red / pair / park)
@@ -286,6 +288,7 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
                 const uint32_t ld = __builtin_amdgcn_readfirstlane(lds0 + slot + 1024u * i);
                 if (dvo[k] != kDrop) dma16<false>(rs_src, dvo[k], so_own, ld);
             } else {
+                if ((TEC_DMA_ABLATE & 64) || ((TEC_DMA_ABLATE & 128) && lvl2)) continue;
                 const uint32_t vo = dvo[k] + (dvo[k] >= skip_from ? skip : 0u);
                 const uint32_t ld = __builtin_amdgcn_readfirstlane(lds0 + slot + kPartBase + 1024u * (i - kOwnInstr));
                 if (dvo[k] != kDrop) {
@@ -320,6 +323,7 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
     asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");  // plane 0 landed (3 <= pieces of plane 1)
 
     uint8_t *const stg = lds8 + kStageBase + colw;
+    uint32_t prev_n = 0;  // ORDER 2: rows this wave stored last step (2 store instructions each)
     for (uint32_t z0 = 0; z0 < (uint32_t)kQ; z0++) {
         const bool lvl2 = z0 >= (uint32_t)K;
         const uint32_t type = lvl2 ? z0 - (K - 1) : 0u;
@@ -406,11 +410,26 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
             // B1: the next plane's DMA has landed (this wave's pieces are older than its last
             // step's >= 2 stores) and every wave is done reading this slot and the staging rows
             if constexpr (!(TEC_DMA_ABLATE & 8)) {
-                if (TEC_DMA_ORDER || z == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                if constexpr (TEC_DMA_ORDER == 2) {
+                    // outstanding, oldest first: the next plane's DMA pieces, then the previous
+                    // step's 2 x prev_n stores -- wait for the DMA only
+                    switch (prev_n) {
+                        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+                        case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+                        case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+                        case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+                        case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+                        default: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+                    }
+                } else if (TEC_DMA_ORDER || z == 0) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                }
             }
             lds_barrier();
-            if (!TEC_DMA_ORDER && z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, slot);
+            if (TEC_DMA_ORDER != 1 && z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, slot);
+            prev_n = (TEC_DMA_ABLATE & 1) ? 0u : n;
 #pragma unroll
             for (int q = 0; q < kCap; q++) {
                 if ((uint32_t)q < n && !(TEC_DMA_ABLATE & 1)) {
@@ -418,7 +437,7 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
                     __builtin_amdgcn_raw_buffer_store_b128(d1[q], rb_dst, (int)vo1, (int)dst[q], TEC_DMA_ST_AUX);
                 }
             }
-            if (TEC_DMA_ORDER && z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, slot);
+            if (TEC_DMA_ORDER == 1 && z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, slot);
         }
     }
     // the last plane's left-over row (its staging row is untouched since the last compute)
@@ -454,14 +473,10 @@ bool encode_dma_supported(int n, int k, uint32_t sc) { return n == 20 && k == 7 
 hipError_t launch_encode_dma(bool masked, const EncArgs &a, hipStream_t s) {
     if (a.njobs == 0) return hipSuccess;
     if (!encode_dma_supported((int)a.n, 7, a.sc) || a.njobs > 0x7fffffffu) return hipErrorInvalidValue;
-    static bool lds_set[2] = {false, false};
     const void *fn = masked ? reinterpret_cast<const void *>(dma::enc_dma_kernel<true>)
                             : reinterpret_cast<const void *>(dma::enc_dma_kernel<false>);
-    if (!lds_set[masked]) {
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dma::kLdsBytes);
-        if (e != hipSuccess) return e;
-        lds_set[masked] = true;
-    }
+    hipError_t e = ensure_dyn_lds(fn, dma::kLdsBytes);
+    if (e != hipSuccess) return e;
     if (masked)
         hipLaunchKernelGGL(dma::enc_dma_kernel<true>, dim3(a.njobs), dim3(dma::G * 64), dma::kLdsBytes, s, a);
     else

@@ -639,13 +639,8 @@ size_t encode_rows_scratch_bytes(const EncArgs &a) {
 template <int K, int G, bool MASKED>
 hipError_t launch_stage_g(const EncArgs &a, uint64_t blocks, hipStream_t s) {
     const size_t lds = stage::lds_bytes(G);
-    static bool lds_set = false;  // per instantiation: raise the dynamic-LDS cap once
-    if (!lds_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(stage::enc_stage_kernel<K, G, MASKED>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        lds_set = true;
-    }
+    hipError_t e = ensure_dyn_lds(reinterpret_cast<const void *>(stage::enc_stage_kernel<K, G, MASKED>), lds);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((stage::enc_stage_kernel<K, G, MASKED>), dim3((uint32_t)blocks), dim3(G * 64), lds, s, a);
     return hipGetLastError();
 }

@@ -35,12 +35,12 @@ constexpr size_t kStripeSizes[3] = {100000, 1000000, 10000000};  // adaptive.rs:
 thread_local char g_last_error[256] = "";
 // TEC_ENCODE_KERNEL=stage selects the previous 1 MB-stripe encode kernel (measurement only)
 const bool g_no_dma_encode = [] {
-    const char *e = getenv("TEC_ENCODE_KERNEL");
+    const char *e = tec_knob("TEC_ENCODE_KERNEL");
     return e && strcmp(e, "stage") == 0;
 }();
 // TEC_REPAIR_KERNEL=stage keeps the folded repair kernel off (measurement / cross-check only)
 const bool g_no_fold_repair = [] {
-    const char *e = getenv("TEC_REPAIR_KERNEL");
+    const char *e = tec_knob("TEC_REPAIR_KERNEL");
     return e && strcmp(e, "stage") == 0;
 }();
 
@@ -328,6 +328,22 @@ struct te_repair_plan {
     std::vector<uint32_t> sub_chunks;   // [ns*d*beta]
 };
 
+namespace tec {
+hipError_t ensure_dyn_lds(const void *fn, size_t bytes) {
+    static std::mutex mu;
+    static std::map<std::pair<int, const void *>, size_t> done;  // (device, kernel) -> limit set
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(mu);
+    size_t &cur = done[{dev, fn}];
+    if (bytes <= cur) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) cur = bytes;
+    return e;
+}
+}  // namespace tec
+
 extern "C" {
 
 const char *te_strerror(int s) {
@@ -359,6 +375,7 @@ const char *te_strerror(int s) {
 int te_device_count(void) { return device_count(); }
 
 const char *te_last_error_detail(void) { return g_last_error; }
+
 
 int te_set_device(int device) {
     if (device < 0 || device >= device_count()) return TE_ERR_NO_DEVICE;
@@ -440,9 +457,13 @@ int te_clay_decode_jit_status(te_clay *c, uint32_t timeout_ms, uint32_t *ready, 
     {
         std::lock_guard<std::mutex> lk(c->mu);
         j = c->jit;
+        if (j) dec_jit_hold(j);  // dec_jit_free (te_clay_free / bind_device, under c->mu) waits for it
     }
     uint32_t r = 0, p = 0, f = 0;
-    if (j) dec_jit_counts(j, timeout_ms, &r, &p, &f);  // j lives until the handle is freed or re-bound
+    if (j) {
+        dec_jit_counts(j, timeout_ms, &r, &p, &f);
+        dec_jit_unhold(j);
+    }
     if (ready) *ready = r;
     if (pending) *pending = p;
     if (failed) *failed = f;
@@ -794,7 +815,7 @@ const te_clay::DecCache *dec_pattern(te_clay *c, uint64_t emask) {
             return (decode_stage_rows(x.nslots, x.max_out) > 53 ? 1u << 20 : 0u) + x.nscratch;
         };
         static const int force = [] {  // TEC_DEC_ORIENT=0/1: one row orientation only (measurement)
-            const char *e = getenv("TEC_DEC_ORIENT");
+            const char *e = tec_knob("TEC_DEC_ORIENT");
             return e ? atoi(e) : -1;
         }();
         for (int orient = 0; orient < 2; orient++) {
@@ -910,13 +931,14 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
             for (const GpeJob &g : kv.second) cnt[g.pattern]++;
             std::vector<int> fx(pats.size(), -1);
             for (size_t p = 0; p < pats.size(); p++) {
-                if (!cnt[p]) continue;
-                const DecJitKernel *k = dec_jit_get(c->jit, h, cached[p]->P, cached[p]->orient, (int)geo.G, (int)geo.wb, cnt[p]);
                 // a pattern kernel gets a launch of its own: only worth it for a group that fills
                 // the GPU; smaller groups stay in the shared table-driven launch (recover's
                 // windows hold ~64 stripes per pattern: 80 small launches per step ran 29.3 ms
-                // against 14.5 for the shared one)
-                if (!k || cnt[p] < jit_floor) continue;
+                // against 14.5 for the shared one).  Such groups do not count toward building a
+                // kernel either: it could never be launched for them.
+                if (cnt[p] < std::max<uint64_t>(1, jit_floor)) continue;
+                const DecJitKernel *k = dec_jit_get(c->jit, h, cached[p]->P, cached[p]->orient, (int)geo.G, (int)geo.wb, cnt[p]);
+                if (!k) continue;
                 fx[p] = (int)fixed.size();
                 fixed.push_back(Fixed{kv.first, k, {}});
             }
@@ -1102,8 +1124,9 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
     const size_t pool_off = A.put(pool.data(), pool.size() * sizeof(uint16_t));
     const size_t pind_off = A.put(pind.data(), pind.size() * sizeof(uint16_t));
     const size_t meta_off = A.put(metas.data(), metas.size() * sizeof(MetaJob));
-    // stripes whose pattern is the all-available one of Clay(20,7,16) go to the folded kernel
-    // (one launch per lost column), the rest to the staged / generic kernel
+    // stripes whose pattern is one of the folded kernel's helper sets of Clay(20,7,16) (all 19
+    // others available, or one of the other column's first 7 down) go to that kernel (one launch
+    // per lost column and set), the rest to the staged / generic kernel
     std::vector<int> fold_col(pats.size(), -1);
     for (size_t i = 0; i < pats.size() && !g_no_fold_repair; i++)
         if (h.nu == 0 && h.n == 2 * h.q)
@@ -1113,7 +1136,8 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
     std::vector<Launch> offs;
     for (auto &kv : groups) {
         const uint32_t sc = (uint32_t)(kv.first / (uint64_t)h.alpha);
-        std::vector<RepJob> part[3];  // fold column 0, fold column 1, other
+        constexpr int kFolds = 16;     // repair_fold.hip kernel indices
+        std::vector<RepJob> part[kFolds + 1];  // folded kernels, then the other stripes
         for (const RepJob &j : kv.second) {
             const int fc = sc >= 8 ? fold_col[j.pattern] : -1;
             RepJob jj = j;
@@ -1124,11 +1148,11 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
                 for (int nd = 0; nd < h.qt; nd++)
                     if (!jj.helper[nd]) jj.helper[nd] = any;
             }
-            part[fc >= 0 ? fc : 2].push_back(jj);
+            part[fc >= 0 ? fc : kFolds].push_back(jj);
         }
-        for (int f = 0; f < 3; f++)
+        for (int f = 0; f <= kFolds; f++)
             if (!part[f].empty())
-                offs.push_back({kv.first, f < 2 ? f : -1, A.put(part[f].data(), part[f].size() * sizeof(RepJob)),
+                offs.push_back({kv.first, f < kFolds ? f : -1, A.put(part[f].data(), part[f].size() * sizeof(RepJob)),
                                 part[f].size()});
     }
     int r = A.upload(s);
@@ -1304,18 +1328,228 @@ static int encode_host_impl(te_clay *c, const te_slicer_cfg *cfg, const uint8_t 
     return rc;
 }
 
-// te_encode_commit_batch_host: encode + commitments, host -> host.  The leaf kernel's time per
-// launch is one slice stream's SHA-256 (~27-30 ms for a 715 KB slice) whatever the
-// number of objects, so hashing must not sit between a window's encode and its D2H copy (hashing
-// each window on its slot stream: 9.6-10.5 GiB/s).  Objects go through the device in GROUPS of at
-// most `window_bytes` (input + output, default 4 GiB); a group's slices stay in one of three
-// resident group buffers (c->pipe[r].out) until hashed.  Each group is encoded in copy windows of
-// <= 128 MiB that rotate over two slot streams like te_encode_batch_host's three (H2D of the
-// window into the slot's input buffer, encode into the group buffer, D2H of its slices: copies stay
-// in stream order behind kernels and overlap across slots).  The handle's stream hashes a whole group
-// at once (one leaf/tree launch per run of equal slice lengths, then the D2H of leaf hashes, roots
-// and proofs) after every slot stream has passed the group's last window, so only the last
-// group's hashing is exposed.  A group buffer is refilled once its hashing is done.
+// te_encode_commit_batch_host / te_stream_submit: encode + commitments, host -> host.  The leaf
+// kernel's time per launch is one slice stream's SHA-256 (~27-30 ms for a 715 KB slice, DESIGN
+// §4.4) whatever the number of objects, so hashing must not sit between a window's encode and its
+// D2H copy (hashing each window on its slot stream: 9.6-10.5 GiB/s).  Objects go through the
+// device in GROUPS of at most `group_bytes` (input + output); a group's slices stay in one of three
+// resident group buffers until hashed.  Each group is encoded in copy windows of <= 128 MiB that
+// rotate over two slot streams (H2D of the window into the slot's input buffer, encode into the
+// group buffer, D2H of its slices: copies stay in stream order behind kernels and overlap across
+// slots).  The hash stream hashes a whole group at once (one leaf/tree launch per run of equal
+// slice lengths, then the D2H of leaf hashes, roots and proofs) after every slot stream has passed
+// the group's last window.  A group buffer is refilled once its hashing is done.  Every ordering
+// is a GPU-side event wait, so the host enqueues a group without blocking: consecutive calls on a
+// CommitPipe (te_stream_submit's windows) overlap one window's encode with the previous one's
+// hashing and copies.
+
+// One device's pipeline state.  The one-shot entry point points it at the handle's slot streams,
+// buffers and arenas (c->pipe, c->stream); a stream writer owns its own (te_stream_writer).
+struct CommitPipe {
+    static constexpr int R = te_clay::kPipe;  // resident group buffers
+    // copy windows rotate over two slot streams: with the hashing stream and the caller's stream
+    // that is four streams for four hardware queues (three slots: 9.5 against 12.0 GiB/s on one
+    // box, 1024 x 4 MiB, in a process that had used its current stream, as bench.py has)
+    static constexpr int S = 2;
+    hipStream_t ss[S] = {}, hs = nullptr;
+    DevBuf *in[S] = {};
+    Arena *arena[S] = {};
+    DevBuf *gout[R] = {}, *gcom[R] = {};
+    // per slot stream "encoded its latest window" and "copied it out", per group buffer "hashed"
+    // (which implies copied out); a stream wait binds to the record current when enqueued
+    hipEvent_t ev_enc[S] = {}, ev_slot[S] = {}, ev_hashed[R] = {};
+    bool slot_used[S] = {}, hashed_pending[R] = {};
+    bool grow_ok = false;  // buffers may grow (after draining their users); else pre-sized
+    size_t w = 0, groups = 0;
+
+    int make_events() {
+        for (hipEvent_t *e : {ev_enc, ev_slot})
+            for (int k = 0; k < S; k++)
+                if (!e[k]) TE_HIP(hipEventCreateWithFlags(&e[k], hipEventDisableTiming));
+        for (int r = 0; r < R; r++)
+            if (!ev_hashed[r]) TE_HIP(hipEventCreateWithFlags(&ev_hashed[r], hipEventDisableTiming));
+        return TE_OK;
+    }
+    void destroy_events() {
+        for (hipEvent_t *e : {ev_enc, ev_slot})
+            for (int k = 0; k < S; k++)
+                if (e[k]) (void)hipEventDestroy(e[k]), e[k] = nullptr;
+        for (int r = 0; r < R; r++)
+            if (ev_hashed[r]) (void)hipEventDestroy(ev_hashed[r]), ev_hashed[r] = nullptr;
+    }
+};
+
+// One call's (or one submitted window's) objects and their commitment outputs.
+struct CommitBatch {
+    const uint8_t *h_data = nullptr;
+    const te_object *objs = nullptr;
+    size_t nobj = 0;
+    uint8_t *h_out = nullptr;
+    CommitOut co{};
+    uint32_t n = 0;
+    std::vector<uint64_t> out_bytes, slice_len;
+    uint64_t leaf_b = 0, proof_b = 0;
+    uint64_t in_bytes(size_t o) const { return (objs[o].blob_len + 15) & ~15ull; }  // device copies 16-byte aligned
+};
+
+static int commit_prepare(const te_clay *c, CommitBatch &B) {
+    B.n = (uint32_t)c->h.n;
+    B.out_bytes.assign(B.nobj, 0);
+    B.slice_len.assign(B.nobj, 0);
+    for (size_t i = 0; i < B.nobj; i++) {
+        te_geometry g;
+        te_slicer_geometry(c, B.objs[i].blob_len, &g);
+        B.slice_len[i] = g.slice_len;
+        B.out_bytes[i] = (uint64_t)B.n * g.slice_len;
+        if (g.slice_len % 4) return TE_ERR_INVALID_ARG;  // the leaf kernel reads dwords
+    }
+    B.leaf_b = (uint64_t)B.n * TE_HASH_SIZE;
+    B.proof_b = B.co.proof ? B.leaf_b * B.co.height : 0;
+    return TE_OK;
+}
+
+// Groups [gcut[x], gcut[x+1]) of about equal size (a small last group would be hashed after the
+// previous one), and each group's copy windows.
+struct CommitPlan {
+    std::vector<size_t> gcut{0};
+    std::vector<std::vector<size_t>> wcut;  // per group: window boundaries, first = group start
+    uint64_t max_win_in = 16, max_group_out = 0, max_group_obj = 0;
+};
+static void commit_plan(const CommitBatch &B, uint64_t group_bytes, uint64_t copy_bytes, CommitPlan &P) {
+    uint64_t total = 0;
+    for (size_t o = 0; o < B.nobj; o++) total += B.objs[o].blob_len + B.out_bytes[o];
+    const uint64_t target = total / std::max<uint64_t>(1, (total + group_bytes - 1) / group_bytes);
+    for (size_t i = 0; i < B.nobj;) {
+        size_t j = i;
+        uint64_t gsz = 0, gout = 0;
+        while (j < B.nobj && (j == i || (gsz < target && gsz + B.objs[j].blob_len + B.out_bytes[j] <= group_bytes))) {
+            gsz += B.objs[j].blob_len + B.out_bytes[j];
+            gout += B.out_bytes[j];
+            j++;
+        }
+        std::vector<size_t> wc{i};
+        for (size_t a = i; a < j;) {
+            size_t b = a;
+            uint64_t win = 0, win_in = 0;
+            while (b < j && (b == a || win + B.objs[b].blob_len + B.out_bytes[b] <= copy_bytes)) {
+                win += B.objs[b].blob_len + B.out_bytes[b];
+                win_in += B.in_bytes(b);
+                b++;
+            }
+            P.max_win_in = std::max(P.max_win_in, win_in + 16);
+            wc.push_back(b);
+            a = b;
+        }
+        P.wcut.push_back(std::move(wc));
+        P.max_group_out = std::max(P.max_group_out, gout);
+        P.max_group_obj = std::max<uint64_t>(P.max_group_obj, j - i);
+        P.gcut.push_back(j);
+        i = j;
+    }
+}
+
+// Enqueue group x of plan L.  `last`: the caller's final group -- its encodes run ahead of the
+// copies (one D2H per two encodes on a slot, the rest after the group's last encode), so its
+// hashing, the only exposed one, starts about halfway through the group's copies.
+static int commit_group(te_clay *c, const te_slicer_cfg *cfg, CommitPipe &P, const CommitBatch &B,
+                        const CommitPlan &L, size_t x, bool last) {
+    constexpr int R = CommitPipe::R, S = CommitPipe::S;
+    const size_t i = L.gcut[x], j = L.gcut[x + 1], r = P.groups % R;
+    const std::vector<size_t> &wc = L.wcut[x];
+    uint64_t gout_bytes = 0, win_in_max = 16;
+    for (size_t o = i; o < j; o++) gout_bytes += B.out_bytes[o];
+    for (size_t y = 0; y + 1 < wc.size(); y++) {
+        uint64_t win_in = 16;
+        for (size_t o = wc[y]; o < wc[y + 1]; o++) win_in += B.in_bytes(o);
+        win_in_max = std::max(win_in_max, win_in);
+    }
+    const uint64_t commit_bytes = (uint64_t)(j - i) * (B.leaf_b + TE_HASH_SIZE + B.proof_b);
+    // buffers: pre-sized by the one-shot path; a stream writer grows one only after the work
+    // queued on it has drained (never under queued work)
+    if (P.gout[r]->cap < gout_bytes || P.gcom[r]->cap < commit_bytes) {
+        if (!P.grow_ok) return TE_ERR_INVALID_ARG;
+        if (P.hashed_pending[r]) TE_HIP(hipEventSynchronize(P.ev_hashed[r]));
+        TE_HIP(P.gout[r]->ensure(gout_bytes));
+        TE_HIP(P.gcom[r]->ensure(commit_bytes));
+    }
+    for (int k = 0; k < S; k++)
+        if (P.in[k]->cap < win_in_max) {
+            if (!P.grow_ok) return TE_ERR_INVALID_ARG;
+            TE_HIP(hipStreamSynchronize(P.ss[k]));
+            TE_HIP(P.in[k]->ensure(win_in_max));
+        }
+    uint8_t *gout = P.gout[r]->as<uint8_t>();
+    if (P.hashed_pending[r])  // the buffer's previous group must be hashed (and, before that, copied out)
+        for (int k = 0; k < S; k++) TE_HIP(hipStreamWaitEvent(P.ss[k], P.ev_hashed[r], 0));
+    std::deque<std::vector<CopyRun>> pend[S];
+    int encs[S] = {};
+    uint64_t dout = 0;
+    std::vector<te_object> local;
+    std::vector<CopyRun> hin, hout;
+    int rc = TE_OK;
+    for (size_t y = 0; y + 1 < wc.size() && !rc; y++) {
+        const size_t a = wc[y], b = wc[y + 1];
+        const int k = (int)(P.w % S);
+        window_layout(B.objs, B.out_bytes, a, b, 0, dout, local, hin, hout);
+        if ((rc = copy_runs(hin, P.in[k]->as<uint8_t>(), B.h_data, hipMemcpyHostToDevice, P.ss[k]))) break;
+        if ((rc = encode_enqueue(c, cfg, P.in[k]->as<uint8_t>(), local.data(), local.size(), gout, P.ss[k], false,
+                                 P.arena[k])))
+            break;
+        if ((rc = hip_status(hipEventRecord(P.ev_enc[k], P.ss[k])))) break;
+        pend[k].push_back(hout);
+        if (!last || ++encs[k] % 2 == 0) {
+            if ((rc = copy_runs(pend[k].front(), gout, B.h_out, hipMemcpyDeviceToHost, P.ss[k]))) break;
+            pend[k].pop_front();
+        }
+        P.slot_used[k] = true;
+        for (size_t o = a; o < b; o++) dout += B.out_bytes[o];
+        P.w++;
+    }
+    for (int k = 0; k < S && !rc; k++) {
+        for (; !pend[k].empty() && !rc; pend[k].pop_front())
+            rc = copy_runs(pend[k].front(), gout, B.h_out, hipMemcpyDeviceToHost, P.ss[k]);
+        if (!rc && P.slot_used[k]) rc = hip_status(hipEventRecord(P.ev_slot[k], P.ss[k]));
+    }
+    if (rc) return rc;
+    // hashing starts once the group is encoded, not copied out: the last windows' D2H overlaps it
+    // (11.9 -> 12.4-12.6 GiB/s, one box)
+    for (int k = 0; k < S; k++)
+        if (P.slot_used[k]) TE_HIP(hipStreamWaitEvent(P.hs, P.ev_enc[k], 0));
+    // commitments of the group's objects, one launch per run of equal slice lengths
+    const uint64_t cnt = j - i, root_at = cnt * B.leaf_b, proof_at = root_at + cnt * TE_HASH_SIZE;
+    uint8_t *dc = P.gcom[r]->as<uint8_t>();
+    uint64_t off = 0;
+    for (size_t o = i; o < j;) {
+        size_t e = o + 1;
+        while (e < j && B.slice_len[e] == B.slice_len[o]) e++;
+        CommitArgs ca{};
+        ca.slices = gout + off;
+        ca.obj_stride = B.out_bytes[o];
+        ca.slice_len = B.slice_len[o];
+        ca.n = B.n;
+        ca.nobj = (uint32_t)(e - o);
+        ca.height = B.co.height;
+        ca.leaf = dc + (o - i) * B.leaf_b;
+        ca.root = dc + root_at + (o - i) * TE_HASH_SIZE;
+        ca.proof = B.co.proof ? dc + proof_at + (o - i) * B.proof_b : nullptr;
+        TE_HIP(launch_commit(ca, P.hs));
+        off += (e - o) * B.out_bytes[o];
+        o = e;
+    }
+    const struct { uint8_t *h; uint64_t d, len; } back[3] = {
+        {B.co.leaf + i * B.leaf_b, 0, cnt * B.leaf_b},
+        {B.co.root + i * TE_HASH_SIZE, root_at, cnt * TE_HASH_SIZE},
+        {B.co.proof ? B.co.proof + i * B.proof_b : nullptr, proof_at, cnt * B.proof_b}};
+    for (const auto &bk : back)
+        if (bk.h && bk.len) TE_HIP(hipMemcpyAsync(bk.h, dc + bk.d, bk.len, hipMemcpyDeviceToHost, P.hs));
+    for (int k = 0; k < S; k++)
+        if (P.slot_used[k]) TE_HIP(hipStreamWaitEvent(P.hs, P.ev_slot[k], 0));
+    TE_HIP(hipEventRecord(P.ev_hashed[r], P.hs));
+    P.hashed_pending[r] = true;
+    P.groups++;
+    return TE_OK;
+}
+
 static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data,
                                    const te_object *objs, size_t nobj, uint8_t *h_out, size_t group_bytes,
                                    const CommitOut &co) {
@@ -1323,169 +1557,118 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
     if (device_count() <= 0) return TE_ERR_NO_DEVICE;
     if (group_bytes == 0) group_bytes = (size_t)4 << 30;
     const uint64_t copy_bytes = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)128 << 20, group_bytes / 8));
-    const uint32_t n = (uint32_t)c->h.n;
-    std::vector<uint64_t> out_bytes(nobj), slice_len(nobj);
-    for (size_t i = 0; i < nobj; i++) {
-        te_geometry g;
-        te_slicer_geometry(c, objs[i].blob_len, &g);
-        slice_len[i] = g.slice_len;
-        out_bytes[i] = (uint64_t)n * g.slice_len;
-        if (g.slice_len % 4) return TE_ERR_INVALID_ARG;  // the leaf kernel reads dwords
-    }
-    auto in_bytes = [&](size_t o) { return (objs[o].blob_len + 15) & ~15ull; };  // device copies 16-byte aligned
-    // plan: groups [gcut[x], gcut[x+1]) and copy windows [wcut[y], wcut[y+1]) inside them
-    // groups of about equal size (a small last group would be hashed after the previous one)
-    std::vector<size_t> gcut{0}, wcut{0};
-    uint64_t total = 0, max_win_in = 16, max_group_out = 0, max_group_obj = 0;
-    for (size_t o = 0; o < nobj; o++) total += objs[o].blob_len + out_bytes[o];
-    const uint64_t target = total / std::max<uint64_t>(1, (total + group_bytes - 1) / group_bytes);
-    for (size_t i = 0; i < nobj;) {
-        size_t j = i;
-        uint64_t gsz = 0, gout = 0;
-        while (j < nobj && (j == i || (gsz < target && gsz + objs[j].blob_len + out_bytes[j] <= group_bytes))) {
-            gsz += objs[j].blob_len + out_bytes[j];
-            gout += out_bytes[j];
-            j++;
-        }
-        for (size_t a = i; a < j;) {
-            size_t b = a;
-            uint64_t win = 0, win_in = 0;
-            while (b < j && (b == a || win + objs[b].blob_len + out_bytes[b] <= copy_bytes)) {
-                win += objs[b].blob_len + out_bytes[b];
-                win_in += in_bytes(b);
-                b++;
-            }
-            max_win_in = std::max(max_win_in, win_in + 16);
-            wcut.push_back(b);
-            a = b;
-        }
-        max_group_out = std::max(max_group_out, gout);
-        max_group_obj = std::max<uint64_t>(max_group_obj, j - i);
-        gcut.push_back(j);
-        i = j;
-    }
-    // per-object commitment bytes (device layout within a group: leaves, then roots, then proofs)
-    const uint64_t leaf_b = (uint64_t)n * TE_HASH_SIZE, proof_b = co.proof ? leaf_b * co.height : 0;
-    const uint64_t commit_cap = max_group_obj * (leaf_b + TE_HASH_SIZE + proof_b);
+    CommitBatch B;
+    B.h_data = h_data;
+    B.objs = objs;
+    B.nobj = nobj;
+    B.h_out = h_out;
+    B.co = co;
+    int rc = commit_prepare(c, B);
+    if (rc) return rc;
+    CommitPlan L;
+    commit_plan(B, group_bytes, copy_bytes, L);
+    const uint64_t commit_cap = L.max_group_obj * (B.leaf_b + TE_HASH_SIZE + B.proof_b);
 
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
     TE_HIP(dg.err);
-    constexpr int P = te_clay::kPipe;
     for (auto &sl : c->pipe)
         if (!sl.s) TE_HIP(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
     // the hashing runs on the handle's own stream (idle here: the handle is locked), so the call
     // uses four streams -- the process's four hardware queues; a fifth stream shared a queue with
     // a slot stream in bench.py (9.5 against 12.1 GiB/s in a process with no other streams)
     if (!c->stream) TE_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    const hipStream_t sh = c->stream;
-    // copy windows rotate over two slot streams: with the hashing stream and the caller's stream
-    // that is four streams for four hardware queues (three slots: 9.5 against 12.0 GiB/s on one
-    // box, 1024 x 4 MiB, in a process that had used its current stream, as bench.py has)
-    constexpr int S = 2;
+    CommitPipe P;
+    P.hs = c->stream;
+    for (int k = 0; k < CommitPipe::S; k++) {
+        P.ss[k] = c->pipe[k].s;
+        P.in[k] = &c->pipe[k].in;
+        P.arena[k] = &c->pipe[k].arena;
+    }
+    for (int r = 0; r < CommitPipe::R; r++) {
+        P.gout[r] = &c->pipe[r].out;
+        P.gcom[r] = &c->pipe[r].commit;
+    }
     // every buffer sized up front (the pipeline never reallocates under queued work)
-    const size_t ngroups = gcut.size() - 1, nring = std::min<size_t>(P, ngroups);
-    for (int k = 0; k < S && nobj; k++) TE_HIP(c->pipe[k].in.ensure(max_win_in));
+    const size_t ngroups = L.gcut.size() - 1, nring = std::min<size_t>(CommitPipe::R, ngroups);
+    for (int k = 0; k < CommitPipe::S && nobj; k++) TE_HIP(P.in[k]->ensure(L.max_win_in));
     for (size_t r = 0; r < nring; r++) {
-        TE_HIP(c->pipe[r].out.ensure(max_group_out));
-        TE_HIP(c->pipe[r].commit.ensure(commit_cap));
+        TE_HIP(P.gout[r]->ensure(L.max_group_out));
+        TE_HIP(P.gcom[r]->ensure(commit_cap));
     }
-    // events: per slot stream "encoded its latest window" and "copied it out", per group buffer
-    // "hashed" (which implies copied out); a stream wait binds to the record current when enqueued
-    hipEvent_t ev[3 * P] = {};
-    int rc = TE_OK;
-    for (auto &e : ev)
-        if (!rc) rc = hip_status(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    hipEvent_t *ev_enc = ev, *ev_slot = ev + P, *ev_hashed = ev + 2 * P;
-    bool slot_used[S] = {};
-    std::vector<te_object> local;
-    std::vector<CopyRun> hin, hout;
-    size_t w = 0;  // global copy-window counter (slot = w % S)
-    for (size_t gi = 0; gi < ngroups && rc == TE_OK; gi++) {
-        const size_t i = gcut[gi], j = gcut[gi + 1], r = gi % P;
-        uint8_t *gout = c->pipe[r].out.as<uint8_t>();
-        if (gi >= P)  // the buffer's previous group must be hashed (and, before that, copied out)
-            for (int k = 0; k < S && !rc; k++) rc = hip_status(hipStreamWaitEvent(c->pipe[k].s, ev_hashed[r], 0));
-        // In the last group the encodes run ahead of the copies (one D2H per two encodes on a slot,
-        // the rest after the group's last encode), so its hashing -- the only exposed one --
-        // starts about halfway through the group's copies instead of at their end.
-        const bool last = gi + 1 == ngroups;
-        std::deque<std::vector<CopyRun>> pend[S];
-        int encs[S] = {};
-        uint64_t dout = 0;
-        while (rc == TE_OK && wcut[w] < j) {
-            const size_t a = wcut[w], b = wcut[w + 1];
-            const int k = (int)(w % S);
-            te_clay::Slot &sl = c->pipe[k];
-            window_layout(objs, out_bytes, a, b, 0, dout, local, hin, hout);
-            if ((rc = copy_runs(hin, sl.in.as<uint8_t>(), h_data, hipMemcpyHostToDevice, sl.s))) break;
-            if ((rc = encode_enqueue(c, cfg, sl.in.as<uint8_t>(), local.data(), local.size(), gout, sl.s, false,
-                                     &sl.arena)))
-                break;
-            if ((rc = hip_status(hipEventRecord(ev_enc[k], sl.s)))) break;
-            pend[k].push_back(hout);
-            if (!last || ++encs[k] % 2 == 0) {
-                if ((rc = copy_runs(pend[k].front(), gout, h_out, hipMemcpyDeviceToHost, sl.s))) break;
-                pend[k].pop_front();
-            }
-            slot_used[k] = true;
-            for (size_t o = a; o < b; o++) dout += out_bytes[o];
-            w++;
-        }
-        for (int k = 0; k < S && !rc; k++) {
-            for (; !pend[k].empty() && !rc; pend[k].pop_front())
-                rc = copy_runs(pend[k].front(), gout, h_out, hipMemcpyDeviceToHost, c->pipe[k].s);
-            if (!rc && slot_used[k]) rc = hip_status(hipEventRecord(ev_slot[k], c->pipe[k].s));
-        }
-        if (rc) break;
-        // hashing starts once the group is encoded, not copied out: the last windows' D2H overlaps
-        // it (11.9 -> 12.4-12.6 GiB/s, one box)
-        for (int k = 0; k < S && !rc; k++)
-            if (slot_used[k]) rc = hip_status(hipStreamWaitEvent(sh, ev_enc[k], 0));
-        if (rc) break;
-        // commitments of the group's objects, one launch per run of equal slice lengths
-        const uint64_t cnt = j - i, root_at = cnt * leaf_b, proof_at = root_at + cnt * TE_HASH_SIZE;
-        uint8_t *dc = c->pipe[r].commit.as<uint8_t>();
-        uint64_t off = 0;
-        for (size_t o = i; o < j && rc == TE_OK;) {
-            size_t e = o + 1;
-            while (e < j && slice_len[e] == slice_len[o]) e++;
-            CommitArgs ca{};
-            ca.slices = gout + off;
-            ca.obj_stride = out_bytes[o];
-            ca.slice_len = slice_len[o];
-            ca.n = n;
-            ca.nobj = (uint32_t)(e - o);
-            ca.height = co.height;
-            ca.leaf = dc + (o - i) * leaf_b;
-            ca.root = dc + root_at + (o - i) * TE_HASH_SIZE;
-            ca.proof = co.proof ? dc + proof_at + (o - i) * proof_b : nullptr;
-            rc = hip_status(launch_commit(ca, sh));
-            off += (e - o) * out_bytes[o];
-            o = e;
-        }
-        if (rc) break;
-        const struct { uint8_t *h; uint64_t d, len; } back[3] = {
-            {co.leaf + i * leaf_b, 0, cnt * leaf_b},
-            {co.root + i * TE_HASH_SIZE, root_at, cnt * TE_HASH_SIZE},
-            {co.proof ? co.proof + i * proof_b : nullptr, proof_at, cnt * proof_b}};
-        for (const auto &bk : back)
-            if (bk.h && bk.len && (rc = hip_status(hipMemcpyAsync(bk.h, dc + bk.d, bk.len, hipMemcpyDeviceToHost, sh))))
-                break;
-        for (int k = 0; k < S && !rc; k++)
-            if (slot_used[k]) rc = hip_status(hipStreamWaitEvent(sh, ev_slot[k], 0));
-        if (!rc) rc = hip_status(hipEventRecord(ev_hashed[r], sh));
-    }
+    rc = P.make_events();
+    for (size_t x = 0; x < ngroups && rc == TE_OK; x++) rc = commit_group(c, cfg, P, B, L, x, x + 1 == ngroups);
     for (auto &sl : c->pipe) {
         const int r2 = hip_status(hipStreamSynchronize(sl.s));
         if (rc == TE_OK) rc = r2;
     }
-    const int r2 = hip_status(hipStreamSynchronize(sh));
+    const int r2 = hip_status(hipStreamSynchronize(P.hs));
     if (rc == TE_OK) rc = r2;
-    for (auto &e : ev)
-        if (e) (void)hipEventDestroy(e);
+    P.destroy_events();
     return rc;
 }
+
+// ------------------------------------------------------------------------------------------
+// te_stream_writer: the ordered, asynchronous window submission of the SDK's stream writer
+// (sdk/src/stream/write.rs:332-362: up to min(cores, 4) chunk encodes in flight, handed on in
+// order through FuturesOrdered), over one or more device-bound handles.  Window t goes to handle
+// (t - 1) mod ncoders and is enqueued there without blocking; each handle's CommitPipe persists
+// across windows, so window t+1's encode overlaps window t's hashing and copies.  te_stream_wait
+// completes windows in submission order.
+// ------------------------------------------------------------------------------------------
+struct te_stream_writer {
+    struct Dev {
+        te_clay *c = nullptr;
+        int device = 0;
+        CommitPipe P;
+        hipStream_t ss[CommitPipe::S] = {}, hs = nullptr;
+        DevBuf in[CommitPipe::S], gout[CommitPipe::R], gcom[CommitPipe::R];
+        Arena arena[CommitPipe::S];
+    };
+    struct Ticket {
+        int dev = -1;
+        hipEvent_t done = nullptr;
+        int rc = TE_OK;
+    };
+    std::vector<std::unique_ptr<Dev>> devs;
+    te_slicer_cfg cfg{};
+    uint32_t height = 0;
+    bool proofs = true;
+    uint64_t group_bytes = 0;
+    std::mutex mu;
+    uint64_t next = 1;                   // next ticket
+    std::map<uint64_t, Ticket> tickets;  // submitted, not yet waited
+};
+
+namespace {
+int writer_drain(te_stream_writer::Dev &d) {
+    DeviceGuard dg(d.device);
+    TE_HIP(dg.err);
+    int rc = TE_OK;
+    for (int k = 0; k < CommitPipe::S; k++)
+        if (d.ss[k]) {
+            const int r = hip_status(hipStreamSynchronize(d.ss[k]));
+            if (!rc) rc = r;
+        }
+    if (d.hs) {
+        const int r = hip_status(hipStreamSynchronize(d.hs));
+        if (!rc) rc = r;
+    }
+    return rc;
+}
+void writer_release(te_stream_writer::Dev &d) {
+    DeviceGuard dg(d.device);
+    (void)writer_drain(d);
+    for (auto &b : d.in) b.release();
+    for (auto &b : d.gout) b.release();
+    for (auto &b : d.gcom) b.release();
+    for (auto &a : d.arena) a.release();
+    d.P.destroy_events();
+    for (auto &s : d.ss)
+        if (s) (void)hipStreamDestroy(s), s = nullptr;
+    if (d.hs) (void)hipStreamDestroy(d.hs), d.hs = nullptr;
+}
+}  // namespace
 
 // ------------------------------------------------------------------------------------------
 // C ABI: compute entry points
@@ -1518,6 +1701,124 @@ int te_encode_commit_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint
     const CommitOut co{h_leaf_hashes, h_roots, h_proofs, height};
     return encode_commit_host_impl(c, cfg, h_data, objs, nobj, h_out, window_bytes, co);
 }
+int te_stream_writer_new(te_clay *const *coders, size_t ncoders, const te_slicer_cfg *cfg, uint32_t height,
+                         size_t group_bytes, te_stream_writer **out) {
+    if (!out) return TE_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (!coders || ncoders == 0 || !cfg || height == 0 || height > TE_MAX_MERKLE_TREE_HEIGHT) return TE_ERR_INVALID_ARG;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    for (size_t i = 0; i < ncoders; i++) {
+        if (!coders[i]) return TE_ERR_INVALID_ARG;
+        const uint32_t n = (uint32_t)coders[i]->h.n;
+        if (n > TE_COMMIT_MAX_LEAVES) return TE_ERR_INVALID_ARG;
+        if (height < 64 && (uint64_t)n > (1ull << height)) return TE_ERR_MERKLE_TREE_FULL;
+    }
+    auto *w = new (std::nothrow) te_stream_writer();
+    if (!w) return TE_ERR_OUT_OF_MEMORY;
+    w->cfg = *cfg;
+    w->height = height;
+    w->group_bytes = group_bytes ? group_bytes : ((size_t)1 << 30);
+    int rc = TE_OK;
+    for (size_t i = 0; i < ncoders && !rc; i++) {
+        auto d = std::make_unique<te_stream_writer::Dev>();
+        d->c = coders[i];
+        d->device = coders[i]->device;
+        DeviceGuard dg(d->device);
+        if ((rc = hip_status(dg.err))) break;
+        for (int k = 0; k < CommitPipe::S && !rc; k++)
+            rc = hip_status(hipStreamCreateWithFlags(&d->ss[k], hipStreamNonBlocking));
+        if (!rc) rc = hip_status(hipStreamCreateWithFlags(&d->hs, hipStreamNonBlocking));
+        CommitPipe &P = d->P;
+        P.hs = d->hs;
+        for (int k = 0; k < CommitPipe::S; k++) {
+            P.ss[k] = d->ss[k];
+            P.in[k] = &d->in[k];
+            P.arena[k] = &d->arena[k];
+        }
+        for (int r = 0; r < CommitPipe::R; r++) {
+            P.gout[r] = &d->gout[r];
+            P.gcom[r] = &d->gcom[r];
+        }
+        P.grow_ok = true;  // buffers grow on demand, after the work queued on them has drained
+        if (!rc) rc = P.make_events();
+        w->devs.push_back(std::move(d));
+    }
+    if (rc) {
+        te_stream_writer_free(w);
+        return rc;
+    }
+    *out = w;
+    return TE_OK;
+}
+
+int te_stream_submit(te_stream_writer *w, const uint8_t *h_data, const te_object *objs, size_t nobj, uint8_t *h_out,
+                     uint8_t *h_leaf_hashes, uint8_t *h_roots, uint8_t *h_proofs, uint64_t *ticket) {
+    if (!w || !ticket || (!objs && nobj) || (nobj && (!h_data || !h_out || !h_leaf_hashes || !h_roots)))
+        return TE_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(w->mu);
+    const uint64_t t = w->next++;
+    *ticket = t;
+    te_stream_writer::Ticket &T = w->tickets[t];
+    T.dev = (int)((t - 1) % w->devs.size());
+    te_stream_writer::Dev &d = *w->devs[(size_t)T.dev];
+    te_clay *c = d.c;
+    CommitBatch B;
+    B.h_data = h_data;
+    B.objs = objs;
+    B.nobj = nobj;
+    B.h_out = h_out;
+    B.co = CommitOut{h_leaf_hashes, h_roots, h_proofs, w->height};
+    int rc = commit_prepare(c, B);
+    if (!rc) {
+        CommitPlan L;
+        const uint64_t copy_bytes = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)128 << 20, w->group_bytes / 8));
+        commit_plan(B, w->group_bytes, copy_bytes, L);
+        std::lock_guard<std::mutex> lk(c->mu);
+        DeviceGuard dg(d.device);
+        rc = c->device != d.device ? TE_ERR_INVALID_ARG : hip_status(dg.err);  // handle re-bound under the writer
+        for (size_t x = 0; x + 1 < L.gcut.size() && !rc; x++) rc = commit_group(c, &w->cfg, d.P, B, L, x, false);
+        if (!rc) rc = hip_status(hipEventCreateWithFlags(&T.done, hipEventDisableTiming));
+        if (!rc) rc = hip_status(hipEventRecord(T.done, d.hs));  // after the window's hashing and copies
+    }
+    T.rc = rc;
+    return rc;
+}
+
+int te_stream_wait(te_stream_writer *w, uint64_t ticket) {
+    if (!w || ticket == 0) return TE_ERR_INVALID_ARG;
+    int first = TE_OK;
+    for (;;) {
+        uint64_t t;
+        te_stream_writer::Ticket T;
+        {
+            std::lock_guard<std::mutex> g(w->mu);
+            if (ticket >= w->next) return TE_ERR_INVALID_ARG;  // never submitted
+            if (w->tickets.empty() || w->tickets.begin()->first > ticket) return first;
+            t = w->tickets.begin()->first;
+            T = w->tickets.begin()->second;
+        }
+        int rc = T.rc;
+        if (T.done) {
+            DeviceGuard dg(w->devs[(size_t)T.dev]->device);
+            const int r = hip_status(hipEventSynchronize(T.done));
+            if (!rc) rc = r;
+            (void)hipEventDestroy(T.done);
+        }
+        {
+            std::lock_guard<std::mutex> g(w->mu);
+            w->tickets.erase(t);
+        }
+        if (!first) first = rc;
+    }
+}
+
+void te_stream_writer_free(te_stream_writer *w) {
+    if (!w) return;
+    if (w->next > 1) (void)te_stream_wait(w, w->next - 1);
+    for (auto &d : w->devs) writer_release(*d);
+    delete w;
+}
+
 int te_encode_batch_host_multi(te_clay *const *coders, size_t ncoders, const te_slicer_cfg *cfg, const uint8_t *h_data,
                                const te_object *objs, size_t nobj, uint8_t *h_out, size_t window_bytes) {
     if (!coders || ncoders == 0 || !cfg || (!objs && nobj)) return TE_ERR_INVALID_ARG;
@@ -1621,7 +1922,7 @@ int te_recover_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t 
     };
     // windows: <= kWinBlob decoded bytes and <= kWinSlices re-encoded slice bytes
     uint64_t kWinBlob = 1ull << 30, kWinSlices = 3ull << 30;
-    if (const char *e = getenv("TEC_RECOVER_WINDOW_BYTES")) {  // tests: force several windows
+    if (const char *e = tec_knob("TEC_RECOVER_WINDOW_BYTES")) {  // tests: force several windows
         const uint64_t v = strtoull(e, nullptr, 10);
         if (v) kWinBlob = kWinSlices = v;
     }

@@ -237,8 +237,7 @@ template <int E>
 static hipError_t launch_gpe_t(const GpeArgs &a, hipStream_t s) {
     const size_t lds = (size_t)2 * E * a.alpha * kGpeWords * 4 + a.alpha * a.t + 16;
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(gpe_kernel<E>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipError_t e = ensure_dyn_lds(reinterpret_cast<const void *>(gpe_kernel<E>), lds);
         if (e != hipSuccess) return e;
     }
     const uint64_t blocks = (uint64_t)a.njobs * a.groups_per_stripe;
@@ -250,8 +249,7 @@ template <int E>
 static hipError_t launch_rep_t(const RepArgs &a, hipStream_t s) {
     const size_t lds = (size_t)E * (a.alpha / a.q) * kGpeWords * 4 + a.alpha * a.t + 16;
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(repair_kernel<E>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipError_t e = ensure_dyn_lds(reinterpret_cast<const void *>(repair_kernel<E>), lds);
         if (e != hipSuccess) return e;
     }
     const uint64_t blocks = (uint64_t)a.njobs * a.groups_per_stripe;

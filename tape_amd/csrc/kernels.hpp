@@ -2,10 +2,24 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "gf.hpp"
 #include "dec_fixed.hpp"
 
 namespace tec {
+
+// Measurement knobs (kernel variants, JIT geometry, forced windows) are read from the environment
+// only when TEC_DEBUG_KNOBS=1 is also set: a stray variable in a production process changes nothing.
+inline const char *tec_knob(const char *name) {
+    const char *on = getenv("TEC_DEBUG_KNOBS");
+    if (!on || on[0] != '1' || on[1] != 0) return nullptr;
+    return getenv(name);
+}
+
+// Raise `fn`'s dynamic-LDS limit to `bytes` on the CURRENT device.  Launchers call it before every
+// launch that needs more than 64 KiB; it calls hipFuncSetAttribute once per (device, kernel) and
+// larger size, under a lock (launchers run on several host threads, one handle per GPU).
+hipError_t ensure_dyn_lds(const void *fn, size_t bytes);
 
 // One stripe of one object for the encode kernels (Slicer::encode, slicer.rs:237-296).
 struct EncJob {
@@ -204,6 +218,10 @@ DecJit *dec_jit_new(int device);
 void dec_jit_free(DecJit *j);
 void dec_jit_set(DecJit *j, int mode, uint64_t min_stripes);  // mode 0 off, 1 async, 2 sync
 void dec_jit_counts(DecJit *j, uint32_t timeout_ms, uint32_t *ready, uint32_t *pending, uint32_t *failed);
+// A status reader keeps `j` alive across dec_jit_counts: hold it while the handle's lock still
+// guards `j`, unhold after.  dec_jit_free wakes held waiters and waits for them to leave.
+void dec_jit_hold(DecJit *j);
+void dec_jit_unhold(DecJit *j);
 // The pattern's kernel for G waves of wb-column lanes if built; counts `stripes` toward building it.
 const DecJitKernel *dec_jit_get(DecJit *j, const ClayHost &h, const GpePattern &P, int orient, int G, int wb, uint64_t stripes);
 // Tile geometry of a pattern kernel for sub-chunk sc: lanes of wb columns, wps words per row,
@@ -259,11 +277,12 @@ hipError_t launch_rs16_encode(const Rs16EncArgs &a, uint32_t segments, hipStream
 hipError_t launch_rs16_decode(const Rs16DecArgs &a, hipStream_t s);
 hipError_t launch_repair(const RepArgs &a, uint32_t max_erased, hipStream_t s);
 hipError_t launch_repair_stage(RepArgs a, hipStream_t s);
-// repair_fold.hip: Clay(20,7,16) with every other node available (the decoding matrix folded per
-// lost column); repair_fold_column() -> 0/1 for such a pattern, else -1
+// repair_fold.hip: Clay(20,7,16) with minimum_to_repair's helper set when at most one of the
+// other column's first 7 nodes is unavailable (the decoding matrix folded per lost column and
+// known set); repair_fold_column() -> kernel index 0..15 for such a pattern, else -1
 int repair_fold_column(uint32_t q, uint32_t t, uint32_t k, uint32_t beta, uint32_t sc, uint32_t lost,
                        uint64_t erased_mask, uint64_t aloof_mask);
-hipError_t launch_repair_fold(int yl, RepArgs a, hipStream_t s);
+hipError_t launch_repair_fold(int fold, RepArgs a, hipStream_t s);
 bool repair_stage_supported(uint32_t q, uint32_t beta, uint32_t sc, uint32_t nerased, uint32_t nknown, uint64_t aloof_mask);
 bool encode_rows_supported(int n, int k, int d);
 size_t encode_rows_scratch_bytes(const EncArgs &a);  // a.njobs, a.groups_per_stripe set

@@ -1,21 +1,24 @@
 // repair_fold.hip -- single-chunk Clay repair with the decoding matrix folded at compile time,
-// for the repair every healthy stripe of Clay(20,7,16) takes: all 19 other chunks available, so
-// ClayCoder::minimum_to_repair (repair.rs:53-70 -> clay_codes) picks the lost node's 9
-// column-mates and the first 7 nodes of the other column, leaving that column's last 3 aloof.
-// The erasure pattern is then fixed by the lost node's column y_l alone; the kernel is
-// instantiated once per column with the MDS decoding matrix D = G_E inv(G_K) as constants.
-// Other helper sets run the table-driven kernel (repair_stage.hip); results are identical.
+// for the helper sets ClayCoder::minimum_to_repair (repair.rs:53-70 -> clay_codes) picks in
+// Clay(20,7,16): the lost node's 9 column-mates plus the first 7 available nodes of the other
+// column.  With all 19 others available (a healthy cluster) those are the other column's nodes
+// 0..6; with one of them down (a peer outage, the node's fallback across peer maps,
+// network/node/src/features/spool/repair.rs:228-267) they are 0..7 without it.  The erasure
+// pattern is then fixed by the lost column y_l and the other column's known set K (7 of 10
+// positions, the other 3 aloof); the kernel is instantiated per (y_l, K) for those 2 x 8 sets
+// with the MDS decoding matrix D = G_E inv(G_K) as constants.  Other helper sets run the
+// table-driven kernel (repair_stage.hip); results are identical.
 //
 // Algebra (Ceph repair_one_lost_chunk): the beta = 10 repair planes are the
 // planes whose y_l digit is x_l; index them by their other digit w (= the row of each helper's
-// repair data).  For known node j (other column, x = j < 7) at plane w:
-//   w == j        red, U = C
-//   w <  7, != j  partner = known node w at plane j: the pair is uncoupled from both C's
-//   w >= 7        partner = aloof node w at plane j: U = a_c C + a_p U_aloof(w, j)
-// so planes 0..6 go first (they also yield the aloof U's planes 7..9 consume).  Per plane the
-// MDS solve gives the 10 column nodes' U: the lost node is red (its C at the plane = U) and each
-// column-mate m's helper C and solved U give the lost chunk at the plane whose y_l digit is x_m.
-// Every plane thus finishes 10 lost-chunk planes (y_l digit 0..9, other digit w).
+// repair data).  For known node j of the other column at plane w:
+//   w == j             red, U = C
+//   w in K, w != j     partner = known node w at plane j: the pair is uncoupled from both C's
+//   w aloof            partner = aloof node w at plane j: U = a_c C + a_p U_aloof(w, j)
+// so the planes w in K go first (they also yield the aloof U's the aloof planes consume).  Per
+// plane the MDS solve gives the 10 column nodes' U: the lost node is red (its C at the plane = U)
+// and each column-mate m's helper C and solved U give the lost chunk at the plane whose y_l digit
+// is x_m.  Every plane thus finishes 10 lost-chunk planes (y_l digit 0..9, other digit w).
 //
 // Work decomposition (MI355X): a workgroup owns one stripe's row segment (G <= 6 waves x 64 lanes
 // x 4 columns), a lane one 4-column word.  The lane loads each helper row it needs exactly once
@@ -37,23 +40,53 @@ namespace rfold {
 constexpr int kQ = 10, kK = 7, kA = kQ - kK;  // known / aloof nodes of the other column
 constexpr int kMaxG = 6;
 
-// D rows: the 10 column nodes (x = 0..9), then the 3 aloof nodes (other column, x = 7..9);
-// columns: the known nodes (other column, x = 0..6).
+// The other column's known set K as a 10-bit mask of positions; its members ascending (kn) and
+// the aloof rest (al).
+struct KSet {
+    int kn[kK], al[kA];
+};
+constexpr KSet make_kset(uint32_t km) {
+    KSet s{};
+    int a = 0, b = 0;
+    for (int x = 0; x < kQ; x++) {
+        if ((km >> x) & 1u) {
+            if (a < kK) s.kn[a] = x;
+            a++;
+        } else {
+            if (b < kA) s.al[b] = x;
+            b++;
+        }
+    }
+    return s;
+}
+constexpr int popc10(uint32_t km) {
+    int c = 0;
+    for (int x = 0; x < kQ; x++) c += (km >> x) & 1u;
+    return c;
+}
+
+// The instantiated known sets: minimum_to_repair's choice with every other node available
+// (0..6), and with other-column node p < 7 unavailable ({0..7} \ {p}).
+constexpr uint32_t kFoldSets[8] = {0x07fu, 0x0feu, 0x0fdu, 0x0fbu, 0x0f7u, 0x0efu, 0x0dfu, 0x0bfu};
+
+// D rows: the 10 column nodes (x = 0..9), then the 3 aloof nodes of the other column (al order);
+// columns: the known nodes of the other column (kn order).
 struct Fold {
     uint8_t D[kQ + kA][kK];
 };
 
-constexpr Fold make_fold(int yl) {
+constexpr Fold make_fold(int yl, uint32_t km) {
     const Mat g = rs_generator(kK, 2 * kQ);
     const int yo = 1 - yl;
+    const KSet ks = make_kset(km);
     Mat gk{};
     gk.rows = gk.cols = kK;
     for (int j = 0; j < kK; j++)
-        for (int c = 0; c < kK; c++) gk.v[j][c] = g.v[yo * kQ + j][c];
+        for (int c = 0; c < kK; c++) gk.v[j][c] = g.v[yo * kQ + ks.kn[j]][c];
     mat_invert(gk);
     Fold f{};
     for (int e = 0; e < kQ + kA; e++) {
-        const int node = e < kQ ? yl * kQ + e : yo * kQ + kK + (e - kQ);
+        const int node = e < kQ ? yl * kQ + e : yo * kQ + ks.al[e - kQ];
         for (int j = 0; j < kK; j++) {
             uint8_t acc = 0;
             for (int l = 0; l < kK; l++) acc ^= gf_mul(g.v[node][l], gk.v[l][j]);
@@ -80,9 +113,9 @@ __device__ __forceinline__ uint32_t half(uint32_t x) {
 __device__ __forceinline__ uint32_t lost_c(uint32_t cm, uint32_t um) { return half(enc::xor3(um, cm, xt(cm))); }
 
 // acc[r] = sum_j D[r][j] u[j] for rows [0, NR) (NR = 13 with the aloof rows, 10 without)
-template <int YL, int NR>
+template <int YL, uint32_t KM, int NR>
 __device__ __forceinline__ void mds(const uint32_t *u, uint32_t *acc) {
-    constexpr Fold F = make_fold(YL);
+    constexpr Fold F = make_fold(YL, KM);
     uint32_t pend[NR];
     bool hp[NR];
 #pragma unroll
@@ -111,9 +144,11 @@ __device__ __forceinline__ void mds(const uint32_t *u, uint32_t *acc) {
         if (hp[r]) acc[r] ^= pend[r];
 }
 
-template <int YL, int G>
+template <int YL, int G, uint32_t KM>
 __global__ void __launch_bounds__(G * 64, 2) rep_fold_kernel(RepArgs a) {
     constexpr int YO = 1 - YL;
+    static_assert(popc10(KM) == kK, "seven known nodes in the other column");
+    constexpr KSet KS = make_kset(KM);
     constexpr uint32_t RS = G * 256u;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint8_t *const lds8 = reinterpret_cast<uint8_t *>(lds);  // 2 x 10 staging rows, 21 aloof-U rows
@@ -179,100 +214,120 @@ __global__ void __launch_bounds__(G * 64, 2) rep_fold_kernel(RepArgs a) {
                 __builtin_amdgcn_raw_buffer_store_b16(*reinterpret_cast<const uint16_t *>(row + lt_off), rs_out, (int)vot, (int)off, 0);
         }
     };
-    // lane-private LDS rows after the staging buffers: aloof node 7 + i's U at plane j < 7
+    // lane-private LDS rows after the staging buffers: aloof node al[i]'s U at plane kn[j]
     auto ua_at = [&](uint32_t i, uint32_t j) {
         return reinterpret_cast<uint32_t *>(lds8 + (2u * kQ + i * kK + j) * RS + col_local);
     };
 
     // Loads of plane p, issued one plane ahead and unconditionally (a branch around a load makes
     // the compiler wait for it inside the branch): the known nodes' C; each one's partner C --
-    // known node p at plane j, the helper row another plane loads as its own, so the re-read is
-    // an L2 hit; at j == p it is the node's own C and pft3(C, C) = C (red); for p >= 7 node p
-    // is aloof and the value is unused; and the column-mates' C (unused for the lost node).
+    // known node p at plane kn[j], the helper row another plane loads as its own, so the re-read
+    // is an L2 hit; at kn[j] == p it is the node's own C and pft3(C, C) = C (red); for aloof p
+    // the value is unused; and the column-mates' C (unused for the lost node).
     uint32_t own[kK], part[kK], cm[kQ];
     auto load_plane = [&](uint32_t p) {
 #pragma unroll
         for (int j = 0; j < kK; j++) {
-            own[j] = load_h(YO * kQ + j, p);
-            part[j] = load_h(YO * kQ + p, j);
+            own[j] = load_h(YO * kQ + KS.kn[j], p);
+            part[j] = load_h(YO * kQ + p, (uint32_t)KS.kn[j]);
         }
 #pragma unroll
         for (int x = 0; x < kQ; x++) cm[x] = load_h(YL * kQ + x, p);
     };
-    load_plane(0);
+    load_plane((uint32_t)KS.kn[0]);
     // Both plane loops are unrolled (no loop-carried register copies, whose moves would wait for
     // the in-flight loads and, vmcnt being in order, for the plane's stores), with a scheduling
     // barrier per plane so the compiler does not hoist every plane's loads to the top.
 #pragma unroll
-    for (uint32_t p = 0; p < (uint32_t)kK; p++) {  // level 1: every known partner is a helper
+    for (int jp = 0; jp < kK; jp++) {  // known planes: every known partner is a helper
+        const uint32_t p = (uint32_t)KS.kn[jp];
         __builtin_amdgcn_sched_barrier(0);
         uint32_t u[kK], ccm[kQ], acc[kQ + kA];
 #pragma unroll
         for (int j = 0; j < kK; j++) u[j] = enc::pft3(own[j], part[j]);
 #pragma unroll
         for (int x = 0; x < kQ; x++) ccm[x] = cm[x];
-        load_plane(p + 1);
-        mds<YL, kQ + kA>(u, acc);
+        load_plane(jp + 1 < kK ? (uint32_t)KS.kn[jp + 1] : (uint32_t)KS.al[0]);
+        mds<YL, KM, kQ + kA>(u, acc);
 #pragma unroll
-        for (int i = 0; i < kA; i++) *ua_at(i, p) = acc[kQ + i];
+        for (int i = 0; i < kA; i++) *ua_at(i, jp) = acc[kQ + i];
         finish(p, acc, ccm);
     }
 #pragma unroll
-    for (uint32_t p = kK; p < (uint32_t)kQ; p++) {  // level 2: partner aloof node p, U from level 1
+    for (int ip = 0; ip < kA; ip++) {  // aloof planes: partner aloof node p, U from the known planes
+        const uint32_t p = (uint32_t)KS.al[ip];
         __builtin_amdgcn_sched_barrier(0);
         uint32_t u[kK], ccm[kQ], acc[kQ];
 #pragma unroll
-        for (int j = 0; j < kK; j++) u[j] = mulc(kPft.a_c[0], own[j]) ^ mulc(kPft.a_p[0], *ua_at(p - kK, j));
+        for (int j = 0; j < kK; j++) u[j] = mulc(kPft.a_c[0], own[j]) ^ mulc(kPft.a_p[0], *ua_at(ip, j));
 #pragma unroll
         for (int x = 0; x < kQ; x++) ccm[x] = cm[x];
-        if (p + 1 < (uint32_t)kQ) load_plane(p + 1);
-        mds<YL, kQ>(u, acc);
+        if (ip + 1 < kA) load_plane((uint32_t)KS.al[ip + 1]);
+        mds<YL, KM, kQ>(u, acc);
         finish(p, acc, ccm);
     }
 }
 
 }  // namespace rfold
 
-// The helper set minimum_to_repair picks with every other node available (Clay(20,7,16)):
-// returns the lost node's column (0/1) when the pattern is that one, else -1.
+// The helper sets of kFoldSets: returns the kernel index (lost column y_l) * 8 + set index for
+// such a pattern, else -1.
 int repair_fold_column(uint32_t q, uint32_t t, uint32_t k, uint32_t beta, uint32_t sc, uint32_t lost,
                        uint64_t erased_mask, uint64_t aloof_mask) {
     using namespace rfold;
     if (q != (uint32_t)kQ || t != 2 || k != (uint32_t)kK || beta != (uint32_t)kQ || sc < 8 || lost >= 2u * kQ) return -1;
     const uint32_t yl = lost / kQ, yo = 1 - yl;
     const uint64_t col = ((1ull << kQ) - 1ull) << (yl * kQ);
-    const uint64_t alf = ((1ull << kA) - 1ull) << (yo * kQ + kK);
-    return (aloof_mask == alf && erased_mask == (col | alf)) ? (int)yl : -1;
+    for (int i = 0; i < 8; i++) {
+        const uint64_t alf = (uint64_t)(~kFoldSets[i] & 0x3ffu) << (yo * kQ);
+        if (aloof_mask == alf && erased_mask == (col | alf)) return (int)yl * 8 + i;
+    }
+    return -1;
 }
 
-template <int YL, int G>
+template <int YL, int G, uint32_t KM>
 static hipError_t launch_fold_g(const RepArgs &a, uint64_t blocks, hipStream_t s) {
     const size_t lds = (size_t)(2 * rfold::kQ + rfold::kA * rfold::kK) * G * 256u;
-    hipLaunchKernelGGL((rfold::rep_fold_kernel<YL, G>), dim3((uint32_t)blocks), dim3(G * 64), lds, s, a);
+    hipLaunchKernelGGL((rfold::rep_fold_kernel<YL, G, KM>), dim3((uint32_t)blocks), dim3(G * 64), lds, s, a);
     return hipGetLastError();
 }
 
-template <int YL>
+template <int YL, uint32_t KM>
 static hipError_t launch_fold_y(const RepArgs &a, uint32_t g, uint64_t blocks, hipStream_t s) {
-    switch (g) {
-        case 1: return launch_fold_g<YL, 1>(a, blocks, s);
-        case 2: return launch_fold_g<YL, 2>(a, blocks, s);
-        case 3: return launch_fold_g<YL, 3>(a, blocks, s);
-        case 4: return launch_fold_g<YL, 4>(a, blocks, s);
-        case 5: return launch_fold_g<YL, 5>(a, blocks, s);
-        default: return launch_fold_g<YL, 6>(a, blocks, s);
+    switch (g) {  // waves per workgroup: sub-chunks below 6 x 256 bytes use fewer
+        case 1: return launch_fold_g<YL, 1, KM>(a, blocks, s);
+        case 2: return launch_fold_g<YL, 2, KM>(a, blocks, s);
+        case 3: return launch_fold_g<YL, 3, KM>(a, blocks, s);
+        case 4: return launch_fold_g<YL, 4, KM>(a, blocks, s);
+        case 5: return launch_fold_g<YL, 5, KM>(a, blocks, s);
+        default: return launch_fold_g<YL, 6, KM>(a, blocks, s);
     }
 }
 
-hipError_t launch_repair_fold(int yl, RepArgs a, hipStream_t s) {
+template <int YL>
+static hipError_t launch_fold_k(int set, const RepArgs &a, uint32_t g, uint64_t blocks, hipStream_t s) {
+    using rfold::kFoldSets;
+    switch (set) {
+        case 0: return launch_fold_y<YL, kFoldSets[0]>(a, g, blocks, s);
+        case 1: return launch_fold_y<YL, kFoldSets[1]>(a, g, blocks, s);
+        case 2: return launch_fold_y<YL, kFoldSets[2]>(a, g, blocks, s);
+        case 3: return launch_fold_y<YL, kFoldSets[3]>(a, g, blocks, s);
+        case 4: return launch_fold_y<YL, kFoldSets[4]>(a, g, blocks, s);
+        case 5: return launch_fold_y<YL, kFoldSets[5]>(a, g, blocks, s);
+        case 6: return launch_fold_y<YL, kFoldSets[6]>(a, g, blocks, s);
+        default: return launch_fold_y<YL, kFoldSets[7]>(a, g, blocks, s);
+    }
+}
+
+hipError_t launch_repair_fold(int fold, RepArgs a, hipStream_t s) {
     if (a.njobs == 0) return hipSuccess;
-    if (a.sc < 8 || (yl != 0 && yl != 1)) return hipErrorInvalidValue;
+    if (a.sc < 8 || fold < 0 || fold >= 16) return hipErrorInvalidValue;
     const uint32_t groups = (a.words_per_stripe + 63) / 64;
     const uint32_t g = groups < (uint32_t)rfold::kMaxG ? groups : (uint32_t)rfold::kMaxG;
     a.wgs_per_stripe = (groups + g - 1) / g;
     const uint64_t blocks = (uint64_t)a.njobs * a.wgs_per_stripe;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    return yl ? launch_fold_y<1>(a, g, blocks, s) : launch_fold_y<0>(a, g, blocks, s);
+    return fold >= 8 ? launch_fold_k<1>(fold - 8, a, g, blocks, s) : launch_fold_k<0>(fold, a, g, blocks, s);
 }
 
 }  // namespace tec

@@ -180,13 +180,8 @@ bool repair_stage_supported(uint32_t q, uint32_t beta, uint32_t sc, uint32_t ner
 template <int G>
 static hipError_t launch_rep_stage_g(const RepArgs &a, uint64_t blocks, hipStream_t s) {
     const size_t lds = rstage::lds_bytes(G);
-    static bool lds_set = false;
-    if (!lds_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(rstage::rep_stage_kernel<13, 10, G>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        lds_set = true;
-    }
+    hipError_t e = ensure_dyn_lds(reinterpret_cast<const void *>(rstage::rep_stage_kernel<13, 10, G>), lds);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((rstage::rep_stage_kernel<13, 10, G>), dim3((uint32_t)blocks), dim3(G * 64), lds, s, a);
     return hipGetLastError();
 }

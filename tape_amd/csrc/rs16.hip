@@ -243,13 +243,8 @@ hipError_t launch_rs16_encode(const Rs16EncArgs &a, uint32_t segments, hipStream
     size_t lds = 0;
     const uint32_t t = rs16_enc_threads(a, &lds);
     if (!t || segments > 65535) return hipErrorInvalidValue;
-    static size_t lds_set = 0;
-    if (lds > lds_set) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(rs16k::rs16_encode_kernel),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        lds_set = lds;
-    }
+    const hipError_t e = ensure_dyn_lds(reinterpret_cast<const void *>(rs16k::rs16_encode_kernel), lds);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rs16k::rs16_encode_kernel, dim3((uint32_t)((a.elems + t - 1) / t), segments), dim3(t), lds, s, a);
     return hipGetLastError();
 }

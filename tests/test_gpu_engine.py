@@ -112,12 +112,14 @@ def test_recover_in_windows(oracle, window):
         off += N * slen
     dev = torch.frombuffer(host, dtype=torch.uint8).cuda()
     out = torch.zeros(out_off, dtype=torch.uint8, device="cuda")
+    os.environ["TEC_DEBUG_KNOBS"] = "1"  # measurement knobs are read only with this set
     os.environ["TEC_RECOVER_WINDOW_BYTES"] = window
     try:
         batch.recover_batch(s, dev, objs, metas, out)
         torch.cuda.synchronize()
     finally:
         del os.environ["TEC_RECOVER_WINDOW_BYTES"]
+        del os.environ["TEC_DEBUG_KNOBS"]
     assert out.cpu().numpy().tobytes() == b"".join(exp)
 
 
@@ -155,6 +157,35 @@ def test_encode_batch_host_multi(oracle):
     got = h_out.numpy()
     for i, L in enumerate(sizes):
         exp = b"".join(oracle.slicer_encode(o, datas[i].tobytes(), chunk_index=i))
+        assert got[out_off[i]:out_off[i] + N * geo[i].slice_len].tobytes() == exp, i
+
+
+@pytest.mark.skipif(T.device_count() < 2, reason="needs two HIP devices")
+def test_encode_batch_host_multi_two_devices(oracle):
+    """The SDK shape of DESIGN §6: one process, one handle per GPU (devices 0 and 1), launched
+    from two host threads at once -- each thread's first launch raises the kernels' LDS limit on
+    its own device (ensure_dyn_lds); bytes equal the oracle's."""
+    import torch
+    s0, s1 = T.Slicer.clay_default(), T.Slicer.clay_default()
+    s1.coder.bind_device(1)
+    assert (s0.coder.device(), s1.coder.device()) == (0, 1)
+    sizes = [4 * MiB, 1_000_003, 4 * MiB, 3_333_333, 2 * MiB + 5, 4 * MiB]
+    geo = [s0.geometry(L) for L in sizes]
+    in_off, out_off, a, b = [], [], 0, 0
+    for L, g in zip(sizes, geo):
+        in_off.append(a)
+        out_off.append(b)
+        a += L
+        b += N * g.slice_len
+    datas = [oracle.splitmix64_bytes(i + 91, L) for i, L in enumerate(sizes)]
+    h_in = torch.from_numpy(np.concatenate(datas)).pin_memory()
+    h_out = torch.zeros(b, dtype=torch.uint8).pin_memory()
+    objs = [(in_off[i], sizes[i], out_off[i], 0) for i in range(len(sizes))]
+    batch.encode_batch_host_multi([s0, s1], h_in, objs, h_out, window_bytes=8 * MiB)
+    o = oracle.OracleClay(20, 7, 16)
+    got = h_out.numpy()
+    for i, L in enumerate(sizes):
+        exp = b"".join(oracle.slicer_encode(o, datas[i].tobytes()))
         assert got[out_off[i]:out_off[i] + N * geo[i].slice_len].tobytes() == exp, i
 
 

@@ -1,0 +1,130 @@
+"""GPU parity of Clay(20,7,16) repair when the helper set is not the all-available one.
+
+A node repairs its slice from whichever peers answer (network/node/src/features/spool/repair.rs:
+228-267, 351-371): with a peer down, ClayCoder::plan_repair (repair.rs:53-70 -> minimum_to_repair)
+still takes the lost node's 9 column-mates but the first 7 *available* nodes of the other column,
+so the aloof set -- and the decoding matrix -- changes.  With one of the other column's first 7
+down the engine runs the folded kernel instantiated for that known set (repair_fold.hip); with two
+down, the table-driven one (repair_stage.hip).  Bar: the repaired slice equals the encoded one,
+byte for byte, and the raw ClayCoder output equals the oracle's chunk.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import tape_amd as T
+
+pytestmark = pytest.mark.gpu
+N = 20
+MiB = 1024 * 1024
+
+
+@pytest.fixture(scope="module")
+def encoded_4mib(oracle):
+    s = T.Slicer.clay_default()
+    data = oracle.splitmix64_bytes(0xD0E5, 4 * MiB).tobytes()
+    return s, s.encode(data)
+
+
+def test_repair_one_peer_down_rotated(encoded_4mib):
+    """Lost slice L, slice L+10 down: under rotation the down shard sits in the other column at the
+    lost shard's position x_l, which moves with the stripe -- every stripe of every L takes either
+    a one-down folded set (x_l < 7) or the all-available one (x_l >= 7)."""
+    s, sl = encoded_4mib
+    for lost in range(N):
+        down = (lost + 10) % N
+        helpers = [(i, sl[i]) for i in range(N) if i not in (lost, down)]
+        assert s.repair_full(lost, helpers) == sl[lost], (lost, down)
+
+
+@pytest.mark.parametrize("lost", [0, 4, 9, 10, 16, 19])
+def test_repair_every_single_down_identity(oracle, lost):
+    """Identity layout (shard = slice): the down node at each position of the other column."""
+    s = T.Slicer.new(T.ClayCoder(20, 7, 16))
+    data = oracle.splitmix64_bytes(0xBEEF ^ lost, 2 * MiB + 333).tobytes()
+    sl = s.encode(data)
+    other = 10 if lost < 10 else 0
+    for p in range(10):
+        down = other + p
+        helpers = [(i, sl[i]) for i in range(N) if i not in (lost, down)]
+        assert s.repair_full(lost, helpers) == sl[lost], (lost, down)
+
+
+def test_repair_two_down_identity(oracle):
+    """Two of the other column down: no folded set, the table-driven kernel; and a column-mate down
+    is minimum_to_repair's error (RepairError::Clay)."""
+    s = T.Slicer.new(T.ClayCoder(20, 7, 16))
+    data = oracle.splitmix64_bytes(77, 3 * MiB).tobytes()
+    sl = s.encode(data)
+    rnd = random.Random(5)
+    for lost in (2, 13):
+        other = 10 if lost < 10 else 0
+        for _ in range(4):
+            downs = rnd.sample(range(other, other + 10), 2)
+            helpers = [(i, sl[i]) for i in range(N) if i != lost and i not in downs]
+            assert s.repair_full(lost, helpers) == sl[lost], (lost, downs)
+        mate = (lost // 10) * 10 + (lost % 10 + 1) % 10
+        with pytest.raises(T.RepairError) as e:
+            s.repair_full(lost, [(i, sl[i]) for i in range(N) if i not in (lost, mate)])
+        assert e.value.variant == "Clay"
+
+
+def test_clay_repair_sets_match_oracle(oracle):
+    """Raw ClayCoder::repair (clay.rs:75-88) for every lost chunk with each single other-column
+    node down: the plan equals the oracle's minimum_to_repair and the chunk equals the encode."""
+    c = T.ClayCoder(20, 7, 16)
+    o = oracle.OracleClay(20, 7, 16)
+    data = oracle.splitmix64_bytes(9, 1_000_000).tobytes()
+    ch = c.encode(data)
+    cs = len(ch[0])
+    sc = cs // c.alpha()
+    for lost in range(N):
+        other = 10 if lost < 10 else 0
+        for p in (0, 3, 6, 8):
+            avail = [i for i in range(N) if i not in (lost, other + p)]
+            plan = c.plan_repair(lost, avail)
+            assert plan == o.minimum_to_repair(lost, avail), (lost, p)
+            helpers = {h: b"".join(ch[h][z * sc:(z + 1) * sc] for z in pl) for h, pl in plan}
+            assert c.repair(lost, helpers, cs) == ch[lost], (lost, p)
+
+
+def test_repair_batch_peer_down(oracle):
+    """te_repair_batch_device over 12 x 4 MiB objects, object i losing slice i mod 20 with slice
+    (i + 10) mod 20 down: one batch mixing the folded kernels of several known sets."""
+    import torch
+    from tape_amd import batch
+    nobj, L = 12, 4 * MiB
+    dev = torch.device("cuda:0")
+    host = np.concatenate([oracle.splitmix64_bytes(0x5EED ^ i, L) for i in range(nobj)])
+    s = T.Slicer.clay_default()
+    g = s.geometry(L)
+    per = N * g.slice_len
+    d_out = torch.zeros(nobj * per, dtype=torch.uint8, device=dev)
+    batch.encode_batch(s, torch.from_numpy(host).to(dev), [(i * L, L, i * per, 0) for i in range(nobj)], d_out)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    plans, offs, blobs, cur, objs = [], [], [], 0, []
+    for i in range(nobj):
+        lost, down = i % N, (i + 10) % N
+        avail = [j for j in range(N) if j not in (lost, down)]
+        p = s.repair_plan_from_params(lost, avail, L, g.stripe_size)
+        o = {}
+        for h in avail:
+            b = T.extract_repair_data(out[i * per + h * g.slice_len:i * per + (h + 1) * g.slice_len].tobytes(), p, h)
+            if b:
+                o[h] = cur
+                blobs.append(b)
+                cur += len(b)
+        plans.append(p)
+        offs.append(o)
+        objs.append((p, o, i * g.slice_len, out[i * per + g.slice_len - 48:i * per + g.slice_len].tobytes()))
+    d_help = torch.from_numpy(np.frombuffer(b"".join(blobs), np.uint8).copy()).to(dev)
+    d_rep = torch.zeros(nobj * g.slice_len, dtype=torch.uint8, device=dev)
+    batch.repair_batch(s.coder, d_help, objs, d_rep)
+    torch.cuda.synchronize()
+    rep = d_rep.cpu().numpy()
+    for i in range(nobj):
+        lost = i % N
+        assert np.array_equal(rep[i * g.slice_len:(i + 1) * g.slice_len],
+                              out[i * per + lost * g.slice_len:i * per + (lost + 1) * g.slice_len]), i

@@ -1,0 +1,117 @@
+"""GPU checks of te_stream_writer: the stream writer's ordered encode stage (sdk/src/stream/
+write.rs:332-362 -- up to min(cores, 4) chunk encodes in flight, handed on in order through
+FuturesOrdered), each window = BlobEncoder::encode_with_proofs of its objects (encoder.rs:220-260).
+
+Several windows are submitted before the first wait; every window's slices equal the oracle's and
+its leaf hashes / roots / proofs the merkle oracle's, and waits complete windows in order.
+"""
+import numpy as np
+import pytest
+
+import tape_amd as T
+from tape_amd import batch
+
+pytestmark = pytest.mark.gpu
+N = 20
+MiB = 1024 * 1024
+H = T.SLICE_TREE_HEIGHT
+
+
+def _window(oracle, s, sizes, seed):
+    import torch
+    geo = [s.geometry(L) for L in sizes]
+    in_off, out_off, a, b = [], [], 0, 0
+    for L, g in zip(sizes, geo):
+        in_off.append(a)
+        out_off.append(b)
+        a += L
+        b += N * g.slice_len
+    datas = [oracle.splitmix64_bytes(seed + i, L) for i, L in enumerate(sizes)]
+    h_in = torch.empty(max(1, a), dtype=torch.uint8).pin_memory()
+    for i, d in enumerate(datas):
+        h_in[in_off[i]:in_off[i] + sizes[i]] = torch.from_numpy(d)
+    nobj = len(sizes)
+    w = {"sizes": sizes, "geo": geo, "datas": datas, "out_off": out_off, "in": h_in,
+         "objs": [(in_off[i], sizes[i], out_off[i], 0) for i in range(nobj)],
+         "out": torch.zeros(max(1, b), dtype=torch.uint8).pin_memory(),
+         "leaf": torch.zeros(nobj * N * 32, dtype=torch.uint8).pin_memory(),
+         "root": torch.zeros(nobj * 32, dtype=torch.uint8).pin_memory(),
+         "proof": torch.zeros(nobj * N * H * 32, dtype=torch.uint8).pin_memory()}
+    return w
+
+
+def _check(oracle, w):
+    from oracle import merkle_oracle as O
+    o = oracle.OracleClay(20, 7, 16)
+    got, lb, rb, pb = (t.numpy().tobytes() for t in (w["out"], w["leaf"], w["root"], w["proof"]))
+    for i, L in enumerate(w["sizes"]):
+        sl_len = w["geo"][i].slice_len
+        exp = oracle.slicer_encode(o, w["datas"][i].tobytes())
+        assert got[w["out_off"][i]:w["out_off"][i] + N * sl_len] == b"".join(exp), i
+        leaves, r, proofs = O.commit_slices(exp, H)
+        assert lb[i * N * 32:(i + 1) * N * 32] == b"".join(leaves), i
+        assert rb[i * 32:(i + 1) * 32] == r, i
+        gp = [[pb[((i * N + j) * H + l) * 32:((i * N + j) * H + l + 1) * 32] for l in range(H)] for j in range(N)]
+        assert gp == proofs, i
+
+
+@pytest.mark.parametrize("handles,group", [(1, 0), (1, 20 * MiB), (2, 0)])
+def test_stream_writer_windows_in_order(oracle, handles, group):
+    """Four windows submitted before the first wait (one or two handles on device 0; small groups
+    split a window into several hashing groups); waiting on ticket 3 completes 1..3 in order."""
+    slicers = [T.Slicer.clay_default() for _ in range(handles)]
+    sw = batch.StreamWriter(slicers, group_bytes=group)
+    wins = [_window(oracle, slicers[0], sizes, 1000 * k) for k, sizes in enumerate(
+        [[4 * MiB] * 3, [1_000_003, 0, 4 * MiB, 77], [3 * MiB + 5] * 4, [2 * MiB, 4 * MiB + 9]])]
+    tickets = [sw.submit(w["in"], w["objs"], w["out"], w["leaf"], w["root"], w["proof"]) for w in wins]
+    assert tickets == [1, 2, 3, 4]
+    sw.wait(3)
+    for w in wins[:3]:
+        _check(oracle, w)
+    sw.wait(4)
+    _check(oracle, wins[3])
+    # the pipeline persists across waits: more windows on the same writer
+    more = [_window(oracle, slicers[0], [4 * MiB, 999], 7000 + k) for k in range(3)]
+    t = [sw.submit(w["in"], w["objs"], w["out"], w["leaf"], w["root"], w["proof"]) for w in more]
+    assert t == [5, 6, 7]
+    sw.wait(7)
+    for w in more:
+        _check(oracle, w)
+    sw.close()
+
+
+def test_stream_writer_without_proofs(oracle):
+    s = T.Slicer.clay_default()
+    sw = batch.StreamWriter([s])
+    w = _window(oracle, s, [4 * MiB, 2 * MiB], 55)
+    t = sw.submit(w["in"], w["objs"], w["out"], w["leaf"], w["root"])
+    sw.wait(t)
+    from oracle import merkle_oracle as O
+    exp = oracle.slicer_encode(oracle.OracleClay(20, 7, 16), w["datas"][0].tobytes())
+    leaves, r, _ = O.commit_slices(exp, H)
+    assert w["leaf"].numpy().tobytes()[:N * 32] == b"".join(leaves)
+    assert w["root"].numpy().tobytes()[:32] == r
+    assert not w["proof"].numpy().any()  # no proofs requested, none written
+    sw.close()
+
+
+@pytest.mark.skipif(T.device_count() < 2, reason="needs two HIP devices")
+def test_stream_writer_two_devices(oracle):
+    s0, s1 = T.Slicer.clay_default(), T.Slicer.clay_default()
+    s1.coder.bind_device(1)
+    sw = batch.StreamWriter([s0, s1])
+    wins = [_window(oracle, s0, [4 * MiB, 3 * MiB], 300 * k) for k in range(4)]
+    for w in wins:
+        sw.submit(w["in"], w["objs"], w["out"], w["leaf"], w["root"], w["proof"])
+    sw.wait(4)
+    for w in wins:
+        _check(oracle, w)
+    sw.close()
+
+
+def test_stream_writer_errors():
+    s = T.Slicer.clay_default()
+    sw = batch.StreamWriter([s])
+    with pytest.raises(T.EngineError):
+        sw.wait(1)  # never submitted
+    sw.close()
