@@ -1,33 +1,114 @@
 //! The reference's `lib/slicer` coders over libtapeec, as INTEGRATION.md describes: a drop-in
-//! `ClayCoder` (clay.rs:13-122), `OuterCoder` (outer.rs:19-197) and the batched write-path call
-//! (`encode_with_proofs` per object, sdk/src/codec/encoder.rs:220-260).  The reference crate's
-//! error enums are restated here with the same variants so this file compiles on its own; inside
-//! lib/slicer the `crate::errors` types replace them.
+//! `ClayCoder` (clay.rs:13-122 + the repair half, repair.rs:49-88) implementing `ErasureCoder`
+//! (coder.rs:14-44), `OuterCoder` (outer.rs:19-197), the `Slicer` whole-object hook
+//! (`slicer_hook`, slicer.rs:237-364) and the batched / streamed write path (`encode_with_proofs`
+//! per object, sdk/src/codec/encoder.rs:220-260; the stream writer's ordered encode stage,
+//! sdk/src/stream/write.rs:332-362).  The reference crate's error enums, `ErasureCoder` trait and
+//! `SliceIndex` are restated here with the same shapes so this file compiles on its own; inside
+//! lib/slicer the `crate::` items replace them.
 //!
 //! Not compiled in this repository's CI (no Rust toolchain in the build image); the FFI it calls
-//! is the generated `tapeec-sys`, which tests/test_rust_binding.py keeps in step with the header.
+//! is the generated `tapeec-sys`, which tests/test_rust_binding.py keeps in step with the header,
+//! and that test also checks every exported `te_clay_*` / `te_slicer_*` / `te_stream_*` entry
+//! point has a caller in this crate.
+use std::collections::HashMap;
 use std::ptr::NonNull;
 use tapeec_sys as ffi;
 
-#[derive(Debug, PartialEq, Eq)]
-pub enum EncodeError { TooMuchData, EmptyInput }
-#[derive(Debug, PartialEq, Eq)]
-pub enum DecodeError { NotEnoughSlices, TooMuchData, BadEncoding, InvalidLayout }
+pub mod slicer_hook;
+pub mod stream;
 
-fn fatal(status: i32) -> ! {
-    let msg = unsafe { std::ffi::CStr::from_ptr(ffi::te_strerror(status)) };
-    let detail = unsafe { std::ffi::CStr::from_ptr(ffi::te_last_error_detail()) };
-    panic!("libtapeec: {} ({})", msg.to_string_lossy(), detail.to_string_lossy())
+#[derive(Clone, Copy, Debug, PartialEq, Eq)]
+pub enum EncodeError { TooMuchData, EmptyInput }
+#[derive(Clone, Copy, Debug, PartialEq, Eq)]
+pub enum DecodeError { NotEnoughSlices, TooMuchData, BadEncoding, InvalidLayout }
+/// errors.rs:28-37
+#[derive(Clone, Debug, PartialEq, Eq)]
+pub enum RepairError {
+    NotEnoughHelpers { needed: u32, available: u32 },
+    InvalidSlice,
+    InvalidLayout(String),
+    Clay(String),
+    MissingHelper(SliceIndex),
 }
 
-/// ClayCoder (lib/slicer/src/clay.rs:13-122) with the GF(2^8) work on the GPU.
-pub struct ClayCoder { raw: NonNull<ffi::te_clay>, pub k: usize, pub m: usize, pub d: usize }
+/// slice_index.rs: a slice / shard position in a spool group.
+#[derive(Clone, Copy, Debug, PartialEq, Eq, Hash, PartialOrd, Ord)]
+pub struct SliceIndex(usize);
+impl SliceIndex {
+    pub fn new(i: usize) -> Self { Self(i) }
+}
+impl std::ops::Deref for SliceIndex {
+    type Target = usize;
+    fn deref(&self) -> &usize { &self.0 }
+}
+
+/// coder.rs:14-44
+pub trait ErasureCoder {
+    fn k(&self) -> usize;
+    fn m(&self) -> usize;
+    fn n(&self) -> usize { self.k() + self.m() }
+    fn encode(&mut self, data: &[u8]) -> Result<Vec<Vec<u8>>, EncodeError>;
+    fn decode(&mut self, chunks: &[(usize, &[u8])]) -> Result<Vec<u8>, DecodeError>;
+}
+
+pub(crate) fn detail() -> String {
+    unsafe { std::ffi::CStr::from_ptr(ffi::te_last_error_detail()) }.to_string_lossy().into_owned()
+}
+
+pub(crate) fn fatal(status: i32) -> ! {
+    let msg = unsafe { std::ffi::CStr::from_ptr(ffi::te_strerror(status)) };
+    panic!("libtapeec: {} ({})", msg.to_string_lossy(), detail())
+}
+
+pub(crate) fn encode_status(s: i32) -> Result<(), EncodeError> {
+    match s {
+        0 => Ok(()),
+        1 => Err(EncodeError::TooMuchData),
+        2 => Err(EncodeError::EmptyInput),
+        s => fatal(s),
+    }
+}
+
+pub(crate) fn decode_status(s: i32) -> Result<(), DecodeError> {
+    match s {
+        0 => Ok(()),
+        3 => Err(DecodeError::NotEnoughSlices),
+        4 => Err(DecodeError::BadEncoding),
+        5 => Err(DecodeError::InvalidLayout),
+        s => fatal(s),
+    }
+}
+
+/// Status -> RepairError, errors.rs:28-37 (detail text from te_last_error_detail, as the
+/// reference's `Clay(e.to_string())` / `InvalidLayout(msg)` carry it).
+pub(crate) fn repair_status(s: i32, missing: Option<SliceIndex>) -> Result<(), RepairError> {
+    match s {
+        0 => Ok(()),
+        6 => {
+            // "not enough helpers: need N, have M" -- the numbers are in the detail text
+            let d = detail();
+            let nums: Vec<u32> = d.split(|c: char| !c.is_ascii_digit()).filter_map(|t| t.parse().ok()).collect();
+            Err(RepairError::NotEnoughHelpers { needed: *nums.first().unwrap_or(&0), available: *nums.get(1).unwrap_or(&0) })
+        }
+        7 => Err(RepairError::InvalidSlice),
+        5 => Err(RepairError::InvalidLayout(detail())),
+        8 => Err(RepairError::Clay(detail())),
+        9 => Err(RepairError::MissingHelper(missing.unwrap_or(SliceIndex(0)))),
+        s => fatal(s),
+    }
+}
+
+/// ClayCoder (lib/slicer/src/clay.rs:13-122) with the GF(2^8) work on the GPU.  The reference's
+/// `pub clay: ClayCode` is never used outside its crate, so it has no counterpart.
+pub struct ClayCoder { pub(crate) raw: NonNull<ffi::te_clay>, pub k: usize, pub m: usize, pub d: usize }
 // libtapeec serialises calls on one handle internally; the handle is bound to its device.
 unsafe impl Send for ClayCoder {}
 
 impl ClayCoder {
+    /// clay.rs:24-34 (same asserts, same messages)
     pub fn new(n: usize, k: usize, d: usize) -> Self {
-        assert!(n > k, "n must be > k"); // clay.rs:24-34
+        assert!(n > k, "n must be > k");
         assert!(k > 0, "k must be > 0");
         assert!(d >= k + 1, "d must be >= k + 1");
         assert!(d <= n - 1, "d must be <= n - 1");
@@ -36,23 +117,109 @@ impl ClayCoder {
         if r != 0 { fatal(r) }
         Self { raw: NonNull::new(p).unwrap(), k, m: n - k, d }
     }
-    pub fn n(&self) -> usize { self.k + self.m }
-    pub fn chunk_size_for(&self, len: usize) -> usize { unsafe { ffi::te_clay_chunk_size_for(self.raw.as_ptr(), len) } }
 
-    pub fn encode(&mut self, data: &[u8]) -> Result<Vec<Vec<u8>>, EncodeError> {
+    /// clay.rs:37-39; `packed` is ClayParams' u64 (n | k << 8 | d << 16, encoding.rs:193-197).
+    pub fn from_params(packed: u64) -> Self {
+        let (n, k, d) = ((packed & 0xff) as usize, ((packed >> 8) & 0xff) as usize, ((packed >> 16) & 0xff) as usize);
+        assert!(n > k && k > 0 && d >= k + 1 && d <= n - 1, "invalid ClayParams");
+        let mut p = std::ptr::null_mut();
+        let r = unsafe { ffi::te_clay_from_params(packed, &mut p) };
+        if r != 0 { fatal(r) }
+        Self { raw: NonNull::new(p).unwrap(), k, m: n - k, d }
+    }
+
+    /// The packed ClayParams of this coder (what the Slicer's profile carries).
+    pub fn params(&self) -> u64 { (self.n() as u64) | (self.k as u64) << 8 | (self.d as u64) << 16 }
+
+    fn info(&self) -> ffi::te_clay_info {
+        let mut i = ffi::te_clay_info { n: 0, k: 0, m: 0, d: 0, q: 0, t: 0, nu: 0, alpha: 0, beta: 0 };
+        let r = unsafe { ffi::te_clay_get_info(self.raw.as_ptr(), &mut i) };
+        if r != 0 { fatal(r) }
+        i
+    }
+    /// clay.rs:42-45
+    pub fn d(&self) -> usize { self.d }
+    /// clay.rs:48-51: sub-chunks per chunk (alpha = q^t)
+    pub fn alpha(&self) -> usize { self.info().alpha as usize }
+    /// clay.rs:54-57: sub-chunks per helper during repair (beta = alpha / q)
+    pub fn beta(&self) -> usize { self.info().beta as usize }
+    /// clay.rs:63-73
+    pub fn chunk_size_for(&self, len: usize) -> usize { unsafe { ffi::te_clay_chunk_size_for(self.raw.as_ptr(), len) } }
+    /// clay.rs:81-84
+    pub fn track_chunk_size(&self, stripe_size: usize, blob_len: usize) -> usize {
+        unsafe { ffi::te_clay_track_chunk_size(self.raw.as_ptr(), stripe_size, blob_len) }
+    }
+
+    /// repair.rs:53-70: (helper shard, sub-chunk indices) per helper, d of them.
+    pub fn plan_repair(&self, lost: SliceIndex, available: &[SliceIndex]) -> Result<Vec<(SliceIndex, Vec<u32>)>, RepairError> {
+        let avail: Vec<u32> = available.iter().map(|s| **s as u32).collect();
+        let (d, beta) = (self.d, self.beta());
+        let mut helpers = vec![0u32; d];
+        let mut subs = vec![0u32; beta];
+        let r = unsafe {
+            ffi::te_clay_plan_repair(self.raw.as_ptr(), *lost as u32, avail.as_ptr(), avail.len(), helpers.as_mut_ptr(),
+                                     subs.as_mut_ptr())
+        };
+        repair_status(r, None)?;
+        // every helper sends the same beta planes
+        Ok(helpers.into_iter().map(|h| (SliceIndex::new(h as usize), subs.clone())).collect())
+    }
+
+    /// repair.rs:75-88: `helpers` maps shard -> its concatenated sub-chunks (plan order).
+    pub fn repair(&self, lost: SliceIndex, helpers: HashMap<SliceIndex, Vec<u8>>, chunk_size: usize) -> Result<Vec<u8>, RepairError> {
+        let mut ids: Vec<u32> = Vec::with_capacity(helpers.len());
+        let mut ptrs: Vec<*const u8> = Vec::with_capacity(helpers.len());
+        for (i, data) in &helpers {
+            ids.push(**i as u32);
+            ptrs.push(data.as_ptr());
+        }
+        let mut out = vec![0u8; chunk_size];
+        let r = unsafe {
+            ffi::te_clay_repair(self.raw.as_ptr(), *lost as u32, ids.as_ptr(), ptrs.as_ptr(), ids.len(), chunk_size,
+                                out.as_mut_ptr())
+        };
+        repair_status(r, None)?;
+        Ok(out)
+    }
+
+    /// The device this coder's work runs on (te_clay_bind_device re-binds it).
+    pub fn device(&self) -> i32 { unsafe { ffi::te_clay_device(self.raw.as_ptr()) } }
+    pub fn bind_device(&mut self, device: i32) {
+        let r = unsafe { ffi::te_clay_bind_device(self.raw.as_ptr(), device) };
+        if r != 0 { fatal(r) }
+    }
+    /// Per-pattern decode kernels (hipRTC): mode 0 off, 1 async, 2 sync.
+    pub fn set_decode_jit(&mut self, mode: i32, min_stripes: u64) {
+        let r = unsafe { ffi::te_clay_set_decode_jit(self.raw.as_ptr(), mode, min_stripes) };
+        if r != 0 { fatal(r) }
+    }
+    /// (ready, compiling, failed) pattern kernels, waiting up to `timeout_ms` for compiles.
+    pub fn decode_jit_status(&self, timeout_ms: u32) -> (u32, u32, u32) {
+        let (mut r, mut p, mut f) = (0u32, 0u32, 0u32);
+        let s = unsafe { ffi::te_clay_decode_jit_status(self.raw.as_ptr(), timeout_ms, &mut r, &mut p, &mut f) };
+        if s != 0 { fatal(s) }
+        (r, p, f)
+    }
+}
+
+impl ErasureCoder for ClayCoder {
+    fn k(&self) -> usize { self.k }
+    fn m(&self) -> usize { self.m }
+
+    /// clay.rs:99-104
+    fn encode(&mut self, data: &[u8]) -> Result<Vec<Vec<u8>>, EncodeError> {
         if data.is_empty() { return Err(EncodeError::EmptyInput) }
         let cs = self.chunk_size_for(data.len());
         let mut buf = vec![0u8; self.n() * cs];
         let mut got = 0usize;
-        match unsafe { ffi::te_clay_encode(self.raw.as_ptr(), data.as_ptr(), data.len(), buf.as_mut_ptr(), buf.len(), &mut got) } {
-            0 => Ok(buf.chunks(got).map(<[u8]>::to_vec).collect()),
-            1 => Err(EncodeError::TooMuchData),
-            2 => Err(EncodeError::EmptyInput),
-            s => fatal(s),
-        }
+        encode_status(unsafe {
+            ffi::te_clay_encode(self.raw.as_ptr(), data.as_ptr(), data.len(), buf.as_mut_ptr(), buf.len(), &mut got)
+        })?;
+        Ok(buf.chunks(got).map(<[u8]>::to_vec).collect())
     }
 
-    pub fn decode(&mut self, chunks: &[(usize, &[u8])]) -> Result<Vec<u8>, DecodeError> {
+    /// clay.rs:106-122
+    fn decode(&mut self, chunks: &[(usize, &[u8])]) -> Result<Vec<u8>, DecodeError> {
         if chunks.len() < self.k { return Err(DecodeError::NotEnoughSlices) }
         let cs = chunks[0].1.len();
         let mut ptrs = vec![std::ptr::null::<u8>(); self.n()];
@@ -61,13 +228,8 @@ impl ClayCoder {
             ptrs[*i] = c.as_ptr();
         }
         let mut out = vec![0u8; self.k * cs];
-        match unsafe { ffi::te_clay_decode(self.raw.as_ptr(), ptrs.as_ptr(), cs, out.as_mut_ptr(), out.len()) } {
-            0 => Ok(out),
-            3 => Err(DecodeError::NotEnoughSlices),
-            5 => Err(DecodeError::InvalidLayout),
-            4 => Err(DecodeError::BadEncoding),
-            s => fatal(s),
-        }
+        decode_status(unsafe { ffi::te_clay_decode(self.raw.as_ptr(), ptrs.as_ptr(), cs, out.as_mut_ptr(), out.len()) })?;
+        Ok(out)
     }
 }
 impl Drop for ClayCoder { fn drop(&mut self) { unsafe { ffi::te_clay_free(self.raw.as_ptr()) } } }
@@ -85,11 +247,10 @@ impl OuterCoder {
         let cb = unsafe { ffi::te_outer_chunk_bytes(self.k as u32, data.len()) };
         let mut out = vec![0u8; self.n * cb];
         let mut got = 0usize;
-        match unsafe { ffi::te_outer_encode(self.k as u32, self.n as u32, data.as_ptr(), data.len(), out.as_mut_ptr(), out.len(), &mut got) } {
-            0 => Ok(out.chunks(cb).map(<[u8]>::to_vec).collect()),
-            1 => Err(EncodeError::TooMuchData),
-            s => fatal(s),
-        }
+        encode_status(unsafe {
+            ffi::te_outer_encode(self.k as u32, self.n as u32, data.as_ptr(), data.len(), out.as_mut_ptr(), out.len(), &mut got)
+        })?;
+        Ok(out.chunks(cb).map(<[u8]>::to_vec).collect())
     }
     pub fn decode(&mut self, chunks: &[(usize, &[u8])]) -> Result<Vec<u8>, DecodeError> {
         if chunks.len() < self.k { return Err(DecodeError::NotEnoughSlices) }
@@ -100,42 +261,55 @@ impl OuterCoder {
             ptrs[*i] = c.as_ptr();
         }
         let mut out = vec![0u8; self.k * cb];
-        match unsafe { ffi::te_outer_decode(self.k as u32, self.n as u32, ptrs.as_ptr(), cb, out.as_mut_ptr(), out.len()) } {
-            0 => Ok(out),
-            3 => Err(DecodeError::NotEnoughSlices),
-            5 => Err(DecodeError::InvalidLayout),
-            s => fatal(s),
-        }
+        decode_status(unsafe {
+            ffi::te_outer_decode(self.k as u32, self.n as u32, ptrs.as_ptr(), cb, out.as_mut_ptr(), out.len())
+        })?;
+        Ok(out)
     }
 }
 
-/// One window of the stream writer (sdk/src/stream/write.rs:332-362): every object's 20 slices
+/// One window of the stream writer (sdk/src/stream/write.rs:332-362): every object's n slices
 /// plus `encode_with_proofs`' leaf hashes, root and proofs, in one call.  Host buffers should be
 /// pinned (hipHostRegister) for full PCIe rate.
 pub struct EncodedWindow { pub slices: Vec<u8>, pub leaf_hashes: Vec<u8>, pub roots: Vec<u8>, pub proofs: Vec<u8> }
 
-pub fn encode_with_proofs_batch(coder: &mut ClayCoder, objects: &[&[u8]], window_bytes: usize)
-        -> Result<EncodedWindow, EncodeError> {
-    let n = coder.n();
-    let cfg = ffi::te_slicer_cfg { rotated: 1, encoding: ffi::TE_ENCODING_CLAY, params: ffi::TE_CLAY_DEFAULT_PARAMS, chunk_index: 0 };
+/// The Slicer configuration of a coder's objects: rotated layout, this coder's ClayParams in the
+/// metadata suffix (not the default profile unless the coder is Clay(20,7,16)).
+pub(crate) fn slicer_cfg(coder: &ClayCoder, rotated: bool, chunk_index: u64) -> ffi::te_slicer_cfg {
+    ffi::te_slicer_cfg { rotated: rotated as i32, encoding: ffi::TE_ENCODING_CLAY, params: coder.params(), chunk_index }
+}
+
+/// Objects laid out back to back (one host buffer, one descriptor each); `chunk_index[o]` is
+/// object o's ChunkNumber salt (0 for SDK user writes, sdk/src/codec/encoder.rs:70-75).
+pub(crate) fn pack_objects(coder: &ClayCoder, objects: &[&[u8]], chunk_index: &[u64]) -> (Vec<u8>, Vec<ffi::te_object>, u64) {
+    let n = coder.n() as u64;
     let mut data = Vec::new();
     let mut objs = Vec::with_capacity(objects.len());
     let mut out_len = 0u64;
-    for o in objects {
+    for (i, o) in objects.iter().enumerate() {
         let mut g = ffi::te_geometry { stripe_size: 0, num_stripes: 0, chunk_size: 0, sub_chunk_size: 0, slice_len: 0 };
         unsafe { ffi::te_slicer_geometry(coder.raw.as_ptr(), o.len(), &mut g) };
-        objs.push(ffi::te_object { data_off: data.len() as u64, blob_len: o.len() as u64, out_off: out_len, chunk_index: 0 });
+        objs.push(ffi::te_object { data_off: data.len() as u64, blob_len: o.len() as u64, out_off: out_len,
+                                   chunk_index: *chunk_index.get(i).unwrap_or(&0) });
         data.extend_from_slice(o);
-        out_len += n as u64 * g.slice_len;
+        out_len += n * g.slice_len;
     }
+    (data, objs, out_len)
+}
+
+pub fn encode_with_proofs_batch(coder: &mut ClayCoder, objects: &[&[u8]], chunk_index: &[u64], window_bytes: usize)
+        -> Result<EncodedWindow, EncodeError> {
+    let n = coder.n();
+    // the metadata suffix names this coder's own profile, not the default one
+    let cfg = slicer_cfg(coder, true, 0);
+    let (data, objs, out_len) = pack_objects(coder, objects, chunk_index);
     let h = ffi::TE_SLICE_TREE_HEIGHT as usize;
     let mut w = EncodedWindow { slices: vec![0; out_len as usize], leaf_hashes: vec![0; objects.len() * n * 32],
                                 roots: vec![0; objects.len() * 32], proofs: vec![0; objects.len() * n * h * 32] };
-    match unsafe { ffi::te_encode_commit_batch_host(coder.raw.as_ptr(), &cfg, data.as_ptr(), objs.as_ptr(), objs.len(),
-                   w.slices.as_mut_ptr(), h as u32, w.leaf_hashes.as_mut_ptr(), w.roots.as_mut_ptr(),
-                   w.proofs.as_mut_ptr(), window_bytes) } {
-        0 => Ok(w),
-        1 => Err(EncodeError::TooMuchData),
-        s => fatal(s),
-    }
+    encode_status(unsafe {
+        ffi::te_encode_commit_batch_host(coder.raw.as_ptr(), &cfg, data.as_ptr(), objs.as_ptr(), objs.len(),
+                                         w.slices.as_mut_ptr(), h as u32, w.leaf_hashes.as_mut_ptr(), w.roots.as_mut_ptr(),
+                                         w.proofs.as_mut_ptr(), window_bytes)
+    })?;
+    Ok(w)
 }

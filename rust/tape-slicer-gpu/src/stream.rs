@@ -1,0 +1,61 @@
+//! The stream writer's ordered encode stage (sdk/src/stream/write.rs:332-362: up to
+//! min(cores, 4) chunk encodes in flight, handed on in order through FuturesOrdered) over
+//! te_stream_writer: one GPU pipeline per ClayCoder (one per device), windows enqueued without
+//! blocking, completed in submission order.  Each window is `encode_with_proofs` of its objects
+//! (sdk/src/codec/encoder.rs:220-260).
+use crate::{encode_status, pack_objects, slicer_cfg, ClayCoder, EncodeError, ErasureCoder};
+use std::collections::BTreeMap;
+use tapeec_sys as ffi;
+
+struct Pending { data: Vec<u8>, objs: Vec<ffi::te_object>, out: crate::EncodedWindow }
+
+pub struct StreamWriter<'a> {
+    raw: *mut ffi::te_stream_writer,
+    coders: Vec<&'a mut ClayCoder>,  // the handles outlive the writer (borrowed)
+    pending: BTreeMap<u64, Pending>,
+}
+
+impl<'a> StreamWriter<'a> {
+    /// group_bytes: hashing group per handle (0 = 1 GiB); height: SLICE_TREE_HEIGHT.
+    pub fn new(coders: Vec<&'a mut ClayCoder>, group_bytes: usize) -> Self {
+        let raws: Vec<*mut ffi::te_clay> = coders.iter().map(|c| c.raw.as_ptr()).collect();
+        let cfg = slicer_cfg(&*coders[0], true, 0);
+        let mut w = std::ptr::null_mut();
+        let r = unsafe {
+            ffi::te_stream_writer_new(raws.as_ptr(), raws.len(), &cfg, ffi::TE_SLICE_TREE_HEIGHT as u32, group_bytes, &mut w)
+        };
+        if r != 0 { crate::fatal(r) }
+        Self { raw: w, coders, pending: BTreeMap::new() }
+    }
+
+    /// Enqueue one window; returns its ticket.  The window's buffers stay owned here (stable
+    /// addresses for the asynchronous copies) until `next` hands them back.
+    pub fn submit(&mut self, objects: &[&[u8]], chunk_index: &[u64]) -> Result<u64, EncodeError> {
+        let (data, objs, out_len) = pack_objects(&*self.coders[0], objects, chunk_index);
+        let n = self.coders[0].n();
+        let h = ffi::TE_SLICE_TREE_HEIGHT as usize;
+        let mut p = Pending { data, objs, out: crate::EncodedWindow {
+            slices: vec![0; out_len as usize], leaf_hashes: vec![0; objects.len() * n * 32],
+            roots: vec![0; objects.len() * 32], proofs: vec![0; objects.len() * n * h * 32] } };
+        let mut t = 0u64;
+        let r = unsafe {
+            ffi::te_stream_submit(self.raw, p.data.as_ptr(), p.objs.as_ptr(), p.objs.len(), p.out.slices.as_mut_ptr(),
+                                  p.out.leaf_hashes.as_mut_ptr(), p.out.roots.as_mut_ptr(), p.out.proofs.as_mut_ptr(), &mut t)
+        };
+        self.pending.insert(t, p);
+        encode_status(r)?;
+        Ok(t)
+    }
+
+    /// The oldest window, completed (FuturesOrdered::next).
+    pub fn next(&mut self) -> Option<Result<crate::EncodedWindow, EncodeError>> {
+        let (&t, _) = self.pending.iter().next()?;
+        let r = unsafe { ffi::te_stream_wait(self.raw, t) };
+        let p = self.pending.remove(&t)?;
+        Some(encode_status(r).map(|_| p.out))
+    }
+}
+
+impl Drop for StreamWriter<'_> {
+    fn drop(&mut self) { unsafe { ffi::te_stream_writer_free(self.raw) } }
+}

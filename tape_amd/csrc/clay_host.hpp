@@ -141,12 +141,18 @@ struct ClayHost {
     // (lane-private LDS if consumed in the same row, per-stripe scratch otherwise).  Follows
     // Ceph decode_layered (oracle/clay_oracle.c decode_layered) value by value; returns false
     // when a dependency would be consumed before it is produced (then the generic engine runs).
-    bool dec_prog(const GpePattern &P, int orient, DecProgHdr &H, std::vector<DecStep> &out) const {
+    //
+    // out_node < 0: the output is the data (Slicer::decode): every data node's C, item x = node.
+    // out_node >= 0: the output is that one node's chunk, item x = 0 (node recover's lost slice,
+    // recover.rs:411-442: a parity node's C comes out of the same layered decode, so nothing is
+    // re-encoded); pairs of erased nodes neither of which is output are skipped either way.
+    bool dec_prog(const GpePattern &P, int orient, DecProgHdr &H, std::vector<DecStep> &out, int out_node = -1) const {
         if (q != kRepQ || t != 2 || nu != 0 || alpha != kRepQ * kRepQ) return false;
         if (P.nknown > (uint32_t)kDecMaxK || P.nerased > (uint32_t)kDecMaxE) return false;
         const uint64_t em = P.erased_mask;
         auto er = [&](int node) { return ((em >> node) & 1ull) != 0; };
-        auto isdata = [&](int node) { return node < k; };
+        auto isdata = [&](int node) { return out_node < 0 ? node < k : node == out_node; };  // an output node
+        const uint32_t relabel = out_node < 0 ? 0xffu : 0u;
         const int yo = orient ? 1 : 0, yi = 1 - yo;
         std::vector<int> rows, cols;
         for (int pass = 0; pass < 2; pass++)
@@ -186,7 +192,7 @@ struct ClayHost {
             for (int i = 0; i < kDecMaxE; i++) S.ek[i] = kErSkip, S.ep[i] = 0, S.ed0[i] = S.ed1[i] = S.epd[i] = kLocNone;
             auto add_out = [&](int node, int plane) -> uint32_t {
                 if (S.nout >= (uint32_t)kDecMaxOut) return kLocNone;
-                S.out[S.nout] = (uint32_t)node | ((uint32_t)plane << 8);
+                S.out[S.nout] = (relabel == 0xffu ? (uint32_t)node : relabel) | ((uint32_t)plane << 8);
                 return (kLocStage << 24) | S.nout++;
             };
             bool ok = true;

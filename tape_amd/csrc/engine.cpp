@@ -277,6 +277,17 @@ struct te_clay {
     int jit_mode = -1;                 // te_clay_set_decode_jit; -1 = the environment's default
     uint64_t jit_min = 0;
     std::unordered_map<uint64_t, DecCache> dec_cache;
+    // Compiled repair patterns by (lost shard, helper shards...): the layered pattern with its
+    // plane lists, the staged kernel's program, and the folded kernel index (-1: none).  Host work
+    // per distinct helper set (matrix inversion, programs) is done once per handle.
+    struct RepCache {
+        RepPattern P;
+        std::vector<uint16_t> pool, pind;
+        RepProg prog{};
+        bool prog_ok = false;
+        int fold = -1;
+    };
+    std::map<std::vector<int>, RepCache> rep_cache;
     struct Slot {
         hipStream_t s = nullptr;
         Arena arena;
@@ -766,6 +777,7 @@ struct DecItem {          // one object, host-validated
     uint64_t in_base;     // offset in d_slices of slice 0
     uint64_t slice_len, blob_len, stripe, ns, cs, out_off;
     uint32_t avail;
+    int32_t lost = -1;    // >= 0: output = that slice's chunks at out_off + stripe * cs (node recover)
 };
 
 // Validate one object like Slicer::decode (slicer.rs:298-331, validate_layout :79-105).
@@ -796,8 +808,10 @@ int decode_validate(const te_clay *c, const uint8_t *meta48, uint64_t slice_len,
 }
 
 // The compiled form of one padded erasure pattern, built once per handle (caller holds c->mu).
-const te_clay::DecCache *dec_pattern(te_clay *c, uint64_t emask) {
-    auto f = c->dec_cache.find(emask);
+// out_node >= 0: the program outputs that internal node's chunk (ClayHost::dec_prog).
+const te_clay::DecCache *dec_pattern(te_clay *c, uint64_t emask, int out_node = -1) {
+    const uint64_t key = emask | (uint64_t)(out_node + 1) << 48;
+    auto f = c->dec_cache.find(key);
     if (f != c->dec_cache.end()) return &f->second;
     const ClayHost &h = c->h;
     const int n = h.n;
@@ -822,7 +836,7 @@ const te_clay::DecCache *dec_pattern(te_clay *c, uint64_t emask) {
             if (force >= 0 && orient != force) continue;
             DecProgHdr H;
             std::vector<DecStep> st;
-            if (!h.dec_prog(d.P, orient, H, st) || !decode_stage_fits(H.nslots, H.max_out)) continue;
+            if (!h.dec_prog(d.P, orient, H, st, out_node) || !decode_stage_fits(H.nslots, H.max_out)) continue;
             if (!found || cost(H) < cost(best)) { best = H; best_steps.swap(st); found = true; d.orient = orient; }
         }
         bool ok = found;
@@ -834,16 +848,19 @@ const te_clay::DecCache *dec_pattern(te_clay *c, uint64_t emask) {
         d.staged = ok;
         d.H = best;
     }
-    return &c->dec_cache.emplace(emask, std::move(d)).first->second;
+    return &c->dec_cache.emplace(key, std::move(d)).first->second;
 }
 
+// Items with lost >= 0 (node recover) need the staged kernel: TE_ERR_UNSUPPORTED, before anything
+// is enqueued, when a pattern has no plane program (the caller then decodes and re-encodes).
 int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices, const DecItem *items,
                    size_t nitems, uint8_t *d_out, hipStream_t s, bool raw) {
     const ClayHost &h = c->h;
     const int n = h.n;
     const int rotated = (cfg && !raw) ? cfg->rotated : 0;
     if (c->dec_cache.size() > 1024) c->dec_cache.clear();  // <= ~27 MB (26 KB per pattern; 77,520 masks exist for k = 7)
-    std::map<uint64_t, uint32_t> pat_index;  // erased mask -> pattern id
+    std::map<uint64_t, uint32_t> pat_index;  // erased mask (| output node << 48) -> pattern id
+    bool fused = false;
     std::vector<GpePattern> pats;
     std::vector<const te_clay::DecCache *> cached;
     std::vector<uint16_t> pool;
@@ -859,26 +876,35 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
                 if (!((it.avail >> sl) & 1u)) emask |= 1ull << h.ext_to_int(sh);
             }
             emask = h.pad_erasures(emask);
-            auto f = pat_index.find(emask);
+            const int onode = it.lost >= 0 ? h.ext_to_int((int)te_slice_to_shard(rotated, (uint32_t)n, (uint32_t)st,
+                                                                                  (uint32_t)it.lost)) : -1;
+            fused = fused || onode >= 0;
+            const uint64_t pkey = emask | (uint64_t)(onode + 1) << 48;
+            auto f = pat_index.find(pkey);
             uint32_t pid;
             if (f == pat_index.end()) {
-                const te_clay::DecCache *dc = dec_pattern(c, emask);
+                const te_clay::DecCache *dc = dec_pattern(c, emask, onode);
                 if (!dc) return TE_ERR_BAD_ENCODING;
                 pid = (uint32_t)pats.size();
                 pats.push_back(dc->P);
                 pats.back().planes_off = (uint32_t)pool.size();
                 pool.insert(pool.end(), dc->planes.begin(), dc->planes.end());
                 cached.push_back(dc);
-                pat_index[emask] = pid;
+                pat_index[pkey] = pid;
                 max_er = std::max(max_er, dc->P.nerased);
             } else {
                 pid = f->second;
             }
             GpeJob g{};
             g.in = d_slices + it.in_base + st * it.cs;
-            g.out = d_out + it.out_off + st * (raw ? 0 : it.stripe);
             g.in_len = ~0ull;
-            g.out_len = raw ? it.cs * (uint64_t)h.k : (st + 1 == it.ns ? it.blob_len - st * it.stripe : it.stripe);
+            if (onode >= 0) {  // the lost slice's chunk of this stripe, whole
+                g.out = d_out + it.out_off + st * it.cs;
+                g.out_len = it.cs;
+            } else {
+                g.out = d_out + it.out_off + st * (raw ? 0 : it.stripe);
+                g.out_len = raw ? it.cs * (uint64_t)h.k : (st + 1 == it.ns ? it.blob_len - st * it.stripe : it.stripe);
+            }
             g.rot = rotated ? (uint32_t)((st * TE_ROTATION_STEP) % n) : 0u;
             g.pattern = pid;
             auto key = (it.cs << 32) ^ it.slice_len;
@@ -911,6 +937,9 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         return staged && sc >= 8 && (uint64_t)n * group_in_stride[key] < 0x7fffffffull &&
                cs * (uint64_t)h.k < 0x7fffffffull;
     };
+    if (fused)
+        for (auto &kv : groups)
+            if (!staged_group(kv.first)) return TE_ERR_UNSUPPORTED;
     // patterns with a per-pattern kernel built (dec_rtc.cpp) leave their group for a launch of
     // their own; every staged stripe counts toward building its pattern's kernel
     struct Fixed { uint64_t key; const DecJitKernel *k; std::vector<GpeJob> jobs; size_t off = 0; };
@@ -918,7 +947,7 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     // a caller that lowered the build threshold (te_clay_set_decode_jit, tests) lowers the floor too
     const uint64_t jit_floor = c->jit_mode >= 0 ? std::min<uint64_t>(kJitMinStripes, c->jit_min) : kJitMinStripes;
     std::vector<Fixed> fixed;
-    if (staged) {
+    if (staged && !fused) {  // (pattern kernels write data chunks; recover's outputs are other nodes)
         if (!c->jit) {
             c->jit = dec_jit_new(c->device);
             if (c->jit_mode >= 0) dec_jit_set(c->jit, c->jit_mode, c->jit_min);
@@ -1065,6 +1094,8 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
     const ClayHost &h = c->h;
     std::map<std::vector<int>, uint32_t> pat_index;  // (lost, helpers...) -> pattern id
     std::vector<RepPattern> pats;
+    std::vector<const te_clay::RepCache *> cached;  // entries stay put: the map is trimmed only here
+    if (c->rep_cache.size() > 4096) c->rep_cache.clear();
     std::vector<uint16_t> pool, pind;
     std::map<uint64_t, std::vector<RepJob>> groups;  // by chunk size
     std::vector<MetaJob> metas;
@@ -1081,12 +1112,26 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
             auto f = pat_index.find(key);
             uint32_t pid;
             if (f == pat_index.end()) {
-                RepPattern P;
-                if (!h.rep_pattern((int)p->lost_shard[st], hs, P, pool, pind)) return TE_ERR_CLAY;
+                auto cf = c->rep_cache.find(key);
+                if (cf == c->rep_cache.end()) {
+                    te_clay::RepCache rc;
+                    if (!h.rep_pattern((int)p->lost_shard[st], hs, rc.P, rc.pool, rc.pind)) return TE_ERR_CLAY;
+                    if (h.nu == 0 && h.n == 2 * h.q && !g_no_fold_repair)
+                        rc.fold = repair_fold_column(h.q, h.t, h.k, rc.P.beta, 8, rc.P.lost, rc.P.erased_mask,
+                                                     rc.P.aloof_mask);
+                    rc.prog_ok = repair_stage_supported(h.q, rc.P.beta, 8, rc.P.nerased, rc.P.nknown, rc.P.aloof_mask) &&
+                                 h.rep_prog(rc.P, rc.pool.data(), rc.pind.data(), rc.prog);
+                    cf = c->rep_cache.emplace(key, std::move(rc)).first;
+                }
+                const te_clay::RepCache &rc = cf->second;
                 pid = (uint32_t)pats.size();
-                pats.push_back(P);
+                pats.push_back(rc.P);
+                pats.back().planes_off = (uint32_t)pool.size();
+                pool.insert(pool.end(), rc.pool.begin(), rc.pool.end());
+                pind.insert(pind.end(), rc.pind.begin(), rc.pind.end());
+                cached.push_back(&rc);
                 pat_index[key] = pid;
-                max_er = std::max(max_er, P.nerased);
+                max_er = std::max(max_er, rc.P.nerased);
             } else {
                 pid = f->second;
             }
@@ -1111,12 +1156,13 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
             metas.push_back(m);
         }
     }
-    // staged kernel when every pattern has a plane program
+    // staged kernel when every pattern outside the folded kernel has a plane program
     std::vector<RepProg> progs(pats.size());
     bool staged = true;
-    for (size_t i = 0; i < pats.size() && staged; i++)
-        staged = repair_stage_supported(h.q, pats[i].beta, 8, pats[i].nerased, pats[i].nknown, pats[i].aloof_mask) &&
-                 h.rep_prog(pats[i], pool.data(), pind.data() + (size_t)i * h.alpha, progs[i]);
+    for (size_t i = 0; i < pats.size(); i++) {
+        progs[i] = cached[i]->prog;
+        if (cached[i]->fold < 0) staged = staged && cached[i]->prog_ok;
+    }
     Arena &A = c->rep;
     A.img.clear();
     const size_t pat_off = A.put(pats.data(), pats.size() * sizeof(RepPattern));
@@ -1128,31 +1174,27 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
     // others available, or one of the other column's first 7 down) go to that kernel (one launch
     // per lost column and set), the rest to the staged / generic kernel
     std::vector<int> fold_col(pats.size(), -1);
-    for (size_t i = 0; i < pats.size() && !g_no_fold_repair; i++)
-        if (h.nu == 0 && h.n == 2 * h.q)
-            fold_col[i] = repair_fold_column(h.q, h.t, h.k, pats[i].beta, 8, pats[i].lost, pats[i].erased_mask,
-                                             pats[i].aloof_mask);
+    for (size_t i = 0; i < pats.size(); i++) fold_col[i] = cached[i]->fold;
     struct Launch { uint64_t cs; int fold; size_t off, njobs; };
     std::vector<Launch> offs;
     for (auto &kv : groups) {
         const uint32_t sc = (uint32_t)(kv.first / (uint64_t)h.alpha);
-        constexpr int kFolds = 16;     // repair_fold.hip kernel indices
-        std::vector<RepJob> part[kFolds + 1];  // folded kernels, then the other stripes
+        std::vector<RepJob> part[2];  // folded (one launch, every kernel index), the other stripes
         for (const RepJob &j : kv.second) {
             const int fc = sc >= 8 ? fold_col[j.pattern] : -1;
             RepJob jj = j;
             if (fc >= 0) {  // the folded kernel loads every node unconditionally (repair_fold.hip)
-                jj.aux = pats[j.pattern].lost % (uint32_t)h.q;
+                jj.aux = pats[j.pattern].lost % (uint32_t)h.q | (uint32_t)fc << 8;
                 const uint8_t *any = nullptr;
                 for (int nd = 0; nd < h.qt && !any; nd++) any = jj.helper[nd];
                 for (int nd = 0; nd < h.qt; nd++)
                     if (!jj.helper[nd]) jj.helper[nd] = any;
             }
-            part[fc >= 0 ? fc : kFolds].push_back(jj);
+            part[fc >= 0 ? 0 : 1].push_back(jj);
         }
-        for (int f = 0; f <= kFolds; f++)
+        for (int f = 0; f < 2; f++)
             if (!part[f].empty())
-                offs.push_back({kv.first, f < kFolds ? f : -1, A.put(part[f].data(), part[f].size() * sizeof(RepJob)),
+                offs.push_back({kv.first, f == 0 ? 0 : -1, A.put(part[f].data(), part[f].size() * sizeof(RepJob)),
                                 part[f].size()});
     }
     int r = A.upload(s);
@@ -1174,7 +1216,7 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
         a.cs = (uint32_t)cs; a.sc = sc; a.q = h.q; a.t = h.t; a.alpha = h.alpha;
         for (int i = 0; i < 16; i++) a.qpow[i] = h.qpow[i];
         if (o.fold >= 0) {
-            TE_HIP(launch_repair_fold(o.fold, a, s));
+            TE_HIP(launch_repair_fold(a, s));
         } else if (staged && sc >= 8) {  // staged kernel: coalesced loads, whole-row stores
             a.progs = A.at<RepProg>(prog_off);
             TE_HIP(launch_repair_stage(a, s));
@@ -1917,6 +1959,53 @@ int te_recover_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t 
         chunk[i] = g.chunk_size;
         for (int w = 0; w < 6; w++) meta_w[i * 6 + w] = get_u64(h_meta + i * TE_META_SIZE + 8 * w);
     }
+    {
+        // Fused: one staged decode whose program outputs only the lost node's chunk of every stripe,
+        // straight into the lost slice -- 7 slices read, 1 written, no decoded object and no
+        // re-encode (a lost parity node's C is produced by the same layered decode).  Empty blobs
+        // have no stripe to decode: their one chunk is zeros.
+        std::vector<DecItem> fi(items);
+        std::vector<CopyJob> zeros;
+        std::vector<MetaJob> metas;
+        for (size_t i = 0; i < nobj; i++) {
+            fi[i].lost = (int32_t)objs[i].lost;
+            fi[i].out_off = objs[i].out_off;
+            uint8_t *dst = d_out + objs[i].out_off;
+            if (items[i].ns == 0) zeros.push_back(CopyJob{d_out, dst, chunk[i] * nstripes[i], 0});
+            MetaJob m{};
+            m.dst = dst + nstripes[i] * chunk[i];
+            m.slice_len = 0;
+            for (int k = 0; k < 6; k++) m.words[k] = meta_w[i * 6 + k];
+            metas.push_back(m);
+        }
+        std::lock_guard<std::mutex> lk(c->mu);
+        DeviceGuard dg(c->device);
+        TE_HIP(dg.err);
+        hipStream_t s = (hipStream_t)stream;
+        const int rf = decode_enqueue(c, cfg, d_slices, fi.data(), nobj, d_out, s, false);
+        if (rf != TE_ERR_UNSUPPORTED) {
+            if (rf) return rf;
+            Arena &A = c->rec;
+            if (c->rec_pending && c->rec_stream != s) TE_HIP(hipStreamWaitEvent(s, c->rec_done, 0));
+            A.img.clear();
+            const size_t zoff = A.put(zeros.data(), zeros.size() * sizeof(CopyJob));
+            const size_t moff = A.put(metas.data(), metas.size() * sizeof(MetaJob));
+            int r = A.upload(s);
+            if (r) return r;
+            KTimer kt(s);
+            if (!zeros.empty()) TE_HIP(launch_gather(A.at<CopyJob>(zoff), (uint32_t)zeros.size(), s));
+            TE_HIP(launch_meta(A.at<MetaJob>(moff), (uint32_t)metas.size(), 1u, s));
+            kt.stop();
+            r = A.mark_done(s);
+            if (!c->rec_done) TE_HIP(hipEventCreateWithFlags(&c->rec_done, hipEventDisableTiming));
+            const int r2 = hip_status(hipEventRecord(c->rec_done, s));
+            c->rec_pending = true;
+            c->rec_stream = s;
+            return r ? r : r2;
+        }
+    }
+    // Otherwise (profiles without plane programs): windowed decode into the object, re-encode of
+    // the parity-lost stripes, gather.
     auto is_parity = [&](size_t i, size_t st) {
         return te_slice_to_shard(rotated, n, (uint32_t)st, objs[i].lost) >= (uint32_t)h.k;
     };

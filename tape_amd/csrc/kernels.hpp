@@ -112,7 +112,7 @@ struct RepJob {
     const uint8_t *helper[kMaxNodes];  // per internal node: this stripe's beta sub-chunks (or null)
     uint8_t *out;                      // lost chunk destination (chunk_size bytes)
     uint32_t pattern;
-    uint32_t aux;                      // repair_fold.hip: x of the lost node
+    uint32_t aux;                      // repair_fold.hip: x of the lost node | kernel index << 8
 };
 
 // Staged repair kernel (repair_stage.hip): per pattern, the uniform control data of every
@@ -279,10 +279,11 @@ hipError_t launch_repair(const RepArgs &a, uint32_t max_erased, hipStream_t s);
 hipError_t launch_repair_stage(RepArgs a, hipStream_t s);
 // repair_fold.hip: Clay(20,7,16) with minimum_to_repair's helper set when at most one of the
 // other column's first 7 nodes is unavailable (the decoding matrix folded per lost column and
-// known set); repair_fold_column() -> kernel index 0..15 for such a pattern, else -1
+// known set); repair_fold_column() -> kernel index 0..15 for such a pattern, else -1.  One launch
+// serves every index: RepJob::aux = x_lost | index << 8.
 int repair_fold_column(uint32_t q, uint32_t t, uint32_t k, uint32_t beta, uint32_t sc, uint32_t lost,
                        uint64_t erased_mask, uint64_t aloof_mask);
-hipError_t launch_repair_fold(int fold, RepArgs a, hipStream_t s);
+hipError_t launch_repair_fold(RepArgs a, hipStream_t s);
 bool repair_stage_supported(uint32_t q, uint32_t beta, uint32_t sc, uint32_t nerased, uint32_t nknown, uint64_t aloof_mask);
 bool encode_rows_supported(int n, int k, int d);
 size_t encode_rows_scratch_bytes(const EncArgs &a);  // a.njobs, a.groups_per_stripe set

@@ -30,6 +30,9 @@
 #include "enc_common.hpp"
 #include "dev_io.hpp"
 
+#ifndef TEC_RFOLD_WPE
+#define TEC_RFOLD_WPE 2  // launch bound: minimum waves per SIMD (register budget)
+#endif
 #ifndef TEC_RFOLD_ST_AUX
 #define TEC_RFOLD_ST_AUX 2  // cache policy of the lost-chunk row stores (nt)
 #endif
@@ -145,7 +148,7 @@ __device__ __forceinline__ void mds(const uint32_t *u, uint32_t *acc) {
 }
 
 template <int YL, int G, uint32_t KM>
-__global__ void __launch_bounds__(G * 64, 2) rep_fold_kernel(RepArgs a) {
+__device__ __forceinline__ void rep_fold_body(const RepArgs &a) {
     constexpr int YO = 1 - YL;
     static_assert(popc10(KM) == kK, "seven known nodes in the other column");
     constexpr KSet KS = make_kset(KM);
@@ -160,7 +163,7 @@ __global__ void __launch_bounds__(G * 64, 2) rep_fold_kernel(RepArgs a) {
     const uint32_t job = tile / a.wgs_per_stripe, seg = tile - job * a.wgs_per_stripe;
     typedef const __attribute__((address_space(4))) RepJob cRepJob;
     cRepJob &J = *(cRepJob *)(uintptr_t)(a.jobs + job);
-    const uint32_t sc = a.sc, wps = a.words_per_stripe, xl = J.aux;
+    const uint32_t sc = a.sc, wps = a.words_per_stripe, xl = J.aux & 0xffu;
     const uint32_t seg0 = seg * RS, lseg = min(RS, sc - seg0);
     uint32_t w = seg * G * 64u + threadIdx.x;
     if (w >= wps) w = wps - 1;
@@ -268,6 +271,33 @@ __global__ void __launch_bounds__(G * 64, 2) rep_fold_kernel(RepArgs a) {
     }
 }
 
+// One launch for every folded stripe of a batch: the job's kernel index (lost column * 8 + set,
+// RepJob::aux >> 8) selects the body; uniform per workgroup, so no divergence (a launch per index
+// ran 0.79 ms against 0.57 for the two launches of the all-available case, 1024 x 4 MiB).
+template <int G>
+__global__ void __launch_bounds__(G * 64, TEC_RFOLD_WPE) rep_fold_kernel(RepArgs a) {
+    const uint32_t job = xcd_tile(blockIdx.x, gridDim.x) / a.wgs_per_stripe;
+    const uint32_t fold = __builtin_amdgcn_readfirstlane(a.jobs[job].aux >> 8);
+    switch (fold) {
+        case 0: rep_fold_body<0, G, kFoldSets[0]>(a); break;
+        case 1: rep_fold_body<0, G, kFoldSets[1]>(a); break;
+        case 2: rep_fold_body<0, G, kFoldSets[2]>(a); break;
+        case 3: rep_fold_body<0, G, kFoldSets[3]>(a); break;
+        case 4: rep_fold_body<0, G, kFoldSets[4]>(a); break;
+        case 5: rep_fold_body<0, G, kFoldSets[5]>(a); break;
+        case 6: rep_fold_body<0, G, kFoldSets[6]>(a); break;
+        case 7: rep_fold_body<0, G, kFoldSets[7]>(a); break;
+        case 8: rep_fold_body<1, G, kFoldSets[0]>(a); break;
+        case 9: rep_fold_body<1, G, kFoldSets[1]>(a); break;
+        case 10: rep_fold_body<1, G, kFoldSets[2]>(a); break;
+        case 11: rep_fold_body<1, G, kFoldSets[3]>(a); break;
+        case 12: rep_fold_body<1, G, kFoldSets[4]>(a); break;
+        case 13: rep_fold_body<1, G, kFoldSets[5]>(a); break;
+        case 14: rep_fold_body<1, G, kFoldSets[6]>(a); break;
+        default: rep_fold_body<1, G, kFoldSets[7]>(a); break;
+    }
+}
+
 }  // namespace rfold
 
 // The helper sets of kFoldSets: returns the kernel index (lost column y_l) * 8 + set index for
@@ -285,49 +315,29 @@ int repair_fold_column(uint32_t q, uint32_t t, uint32_t k, uint32_t beta, uint32
     return -1;
 }
 
-template <int YL, int G, uint32_t KM>
+template <int G>
 static hipError_t launch_fold_g(const RepArgs &a, uint64_t blocks, hipStream_t s) {
     const size_t lds = (size_t)(2 * rfold::kQ + rfold::kA * rfold::kK) * G * 256u;
-    hipLaunchKernelGGL((rfold::rep_fold_kernel<YL, G, KM>), dim3((uint32_t)blocks), dim3(G * 64), lds, s, a);
+    hipLaunchKernelGGL((rfold::rep_fold_kernel<G>), dim3((uint32_t)blocks), dim3(G * 64), lds, s, a);
     return hipGetLastError();
 }
 
-template <int YL, uint32_t KM>
-static hipError_t launch_fold_y(const RepArgs &a, uint32_t g, uint64_t blocks, hipStream_t s) {
-    switch (g) {  // waves per workgroup: sub-chunks below 6 x 256 bytes use fewer
-        case 1: return launch_fold_g<YL, 1, KM>(a, blocks, s);
-        case 2: return launch_fold_g<YL, 2, KM>(a, blocks, s);
-        case 3: return launch_fold_g<YL, 3, KM>(a, blocks, s);
-        case 4: return launch_fold_g<YL, 4, KM>(a, blocks, s);
-        case 5: return launch_fold_g<YL, 5, KM>(a, blocks, s);
-        default: return launch_fold_g<YL, 6, KM>(a, blocks, s);
-    }
-}
-
-template <int YL>
-static hipError_t launch_fold_k(int set, const RepArgs &a, uint32_t g, uint64_t blocks, hipStream_t s) {
-    using rfold::kFoldSets;
-    switch (set) {
-        case 0: return launch_fold_y<YL, kFoldSets[0]>(a, g, blocks, s);
-        case 1: return launch_fold_y<YL, kFoldSets[1]>(a, g, blocks, s);
-        case 2: return launch_fold_y<YL, kFoldSets[2]>(a, g, blocks, s);
-        case 3: return launch_fold_y<YL, kFoldSets[3]>(a, g, blocks, s);
-        case 4: return launch_fold_y<YL, kFoldSets[4]>(a, g, blocks, s);
-        case 5: return launch_fold_y<YL, kFoldSets[5]>(a, g, blocks, s);
-        case 6: return launch_fold_y<YL, kFoldSets[6]>(a, g, blocks, s);
-        default: return launch_fold_y<YL, kFoldSets[7]>(a, g, blocks, s);
-    }
-}
-
-hipError_t launch_repair_fold(int fold, RepArgs a, hipStream_t s) {
+hipError_t launch_repair_fold(RepArgs a, hipStream_t s) {
     if (a.njobs == 0) return hipSuccess;
-    if (a.sc < 8 || fold < 0 || fold >= 16) return hipErrorInvalidValue;
+    if (a.sc < 8) return hipErrorInvalidValue;
     const uint32_t groups = (a.words_per_stripe + 63) / 64;
     const uint32_t g = groups < (uint32_t)rfold::kMaxG ? groups : (uint32_t)rfold::kMaxG;
     a.wgs_per_stripe = (groups + g - 1) / g;
     const uint64_t blocks = (uint64_t)a.njobs * a.wgs_per_stripe;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    return fold >= 8 ? launch_fold_k<1>(fold - 8, a, g, blocks, s) : launch_fold_k<0>(fold, a, g, blocks, s);
+    switch (g) {  // waves per workgroup: sub-chunks below 6 x 256 bytes use fewer
+        case 1: return launch_fold_g<1>(a, blocks, s);
+        case 2: return launch_fold_g<2>(a, blocks, s);
+        case 3: return launch_fold_g<3>(a, blocks, s);
+        case 4: return launch_fold_g<4>(a, blocks, s);
+        case 5: return launch_fold_g<5>(a, blocks, s);
+        default: return launch_fold_g<6>(a, blocks, s);
+    }
 }
 
 }  // namespace tec

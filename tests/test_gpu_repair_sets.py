@@ -128,3 +128,54 @@ def test_repair_batch_peer_down(oracle):
         lost = i % N
         assert np.array_equal(rep[i * g.slice_len:(i + 1) * g.slice_len],
                               out[i * per + lost * g.slice_len:i * per + (lost + 1) * g.slice_len]), i
+
+
+# ---------------------------------------------------------------- node recover ----------------
+@pytest.mark.parametrize("params", [(20, 7, 16), (20, 10, 19), (20, 8, 17), (12, 8, 11)])
+def test_recover_every_lost_node(oracle, params):
+    """te_recover_batch_device = recover.rs:411-442 `reconstruct` for every lost slice: q = 10,
+    t = 2 profiles run the fused decode whose program outputs the lost node's chunk directly (data
+    or parity); (12,8,11) has no plane program and takes the decode + re-encode path.  Peers are
+    exactly k random slices, or all others."""
+    from tape_amd import batch
+    n, k, _ = params
+    s = T.Slicer.with_profile(T.ClayCoder(*params), 1_000_000, True, T.EncodingProfile.clay(T.ClayParams.new(*params)))
+    data = oracle.splitmix64_bytes(sum(params), 2_345_678).tobytes()
+    sl = s.encode(data)
+    rnd = random.Random(n * k)
+    for lost in range(n):
+        for nav in (k, n - 1):
+            avail = sorted(rnd.sample([i for i in range(n) if i != lost], nav))
+            s2 = T.Slicer.with_profile(T.ClayCoder(*params), 1_000_000, True, T.EncodingProfile.clay(T.ClayParams.new(*params)))
+            assert batch.reconstruct(s2, lost, [(i, sl[i]) for i in avail]) == sl[lost], (lost, avail)
+
+
+def test_recover_batch_4mib_random_peers(oracle):
+    """12 x 4 MiB objects, each losing a random slice and keeping 7 random peers (the node's
+    fetch_slices shape, recover.rs:279-408), in one fused launch."""
+    import torch
+    from tape_amd import batch
+    nobj, L = 12, 4 * MiB
+    s = T.Slicer.clay_default()
+    g = s.geometry(L)
+    per = N * g.slice_len
+    host = np.concatenate([oracle.splitmix64_bytes(0xAB ^ i, L) for i in range(nobj)])
+    d_in = torch.from_numpy(host).cuda()
+    d_sl = torch.zeros(nobj * per, dtype=torch.uint8, device="cuda")
+    batch.encode_batch(s, d_in, [(i * L, L, i * per, 0) for i in range(nobj)], d_sl)
+    torch.cuda.synchronize()
+    out = d_sl.cpu().numpy()
+    rnd = random.Random(77)
+    objs, metas, exp = [], b"", []
+    for i in range(nobj):
+        lost = rnd.randrange(N)
+        avail = rnd.sample([j for j in range(N) if j != lost], 7)
+        objs.append((i * per, g.slice_len, sum(1 << j for j in avail), lost, i * g.slice_len))
+        metas += out[i * per + g.slice_len - 48:i * per + g.slice_len].tobytes()
+        exp.append(out[i * per + lost * g.slice_len:i * per + (lost + 1) * g.slice_len])
+    d_rec = torch.zeros(nobj * g.slice_len, dtype=torch.uint8, device="cuda")
+    batch.recover_batch(s, d_sl, objs, metas, d_rec)
+    torch.cuda.synchronize()
+    got = d_rec.cpu().numpy()
+    for i in range(nobj):
+        assert np.array_equal(got[i * g.slice_len:(i + 1) * g.slice_len], exp[i]), i
