@@ -90,6 +90,7 @@ KERNELS = {
     "repair": ["tec::rfold::rep_fold_kernel"],  # every folded instance (lost column x known set)
     "decode": ["tec_dec_fixed"],  # the pattern kernels (dec_rtc.cpp); --decode-jit off: dec_stage_kernel<7, 6>
     "commit": ["tec::commit::leaf_kernel", "tec::commit::tree_kernel"],
+    "recover": ["tec::dstage::dec_stage_kernel<7, 6>"],  # the fused decode writing only the lost slices
 }
 
 
@@ -133,6 +134,9 @@ def main():
     ap.add_argument("--decode-jit", choices=["async", "off"], default="async",
                     help="decode / recover: per-pattern decode kernels (hipRTC-built during warm-up) or "
                          "the table-driven kernel only")
+    ap.add_argument("--pattern", choices=["worst", "random"], default="worst",
+                    help="--mode decode: worst = slices 0..12 erased (config 4); random = each object "
+                         "keeps 7 random slices (the sdk downloader's first-k shape, downloader.rs:79-109)")
     ap.add_argument("--unavailable", type=int, default=0, choices=[0, 1],
                     help="--mode repair: 1 = slice (lost + 10) mod 20 is down too, so every stripe's "
                          "helper set skips one node of the other column (a peer outage)")
@@ -174,8 +178,13 @@ def main():
     if args.mode == "decode":
         metas = b"".join(d_out[i * per + g.slice_len - 48:i * per + g.slice_len].cpu().numpy().tobytes()
                          for i in range(nobj))
-        mask = sum(1 << j for j in range(13, 20))
-        dec_objs = batch.decode_descs([(i * per, g.slice_len, mask, i * L) for i in range(nobj)])
+        if args.pattern == "random":
+            import random
+            rnd = random.Random(0x5EED + first)
+            masks = [sum(1 << j for j in rnd.sample(range(N), 7)) for _ in range(nobj)]
+        else:
+            masks = [sum(1 << j for j in range(13, 20))] * nobj
+        dec_objs = batch.decode_descs([(i * per, g.slice_len, masks[i], i * L) for i in range(nobj)])
         d_dec = torch.empty(nobj * L, dtype=torch.uint8, device=dev)
 
         def step():
@@ -345,9 +354,10 @@ def main():
             "config": {"workload": {"encode": "Slicer::encode",
                                     "repair": "Slicer::repair (lost = i mod 20" +
                                               (", slice (i + 10) mod 20 down)" if args.unavailable else ")"),
-                                    "decode": "Slicer::decode (slices 0..12 erased)",
+                                    "decode": "Slicer::decode (slices 0..12 erased)" if args.pattern == "worst" else
+                                              "Slicer::decode (7 random slices kept per object)",
                                     "commit": "encode_with_proofs commitment (SHA-256 leaf per slice, height-5 root, 20 proofs)",
-                                    "recover": "node recover (decode from 7 slices + re-encode, lost = i mod 20)"}[args.mode]
+                                    "recover": "node recover (the lost slice rebuilt from 7 peer slices, lost = i mod 20)"}[args.mode]
                        + f" of {nobj} x {L} B objects per GPU, Clay(20,7,16) rotated, 1 MB stripes",
                        "objects_per_gpu": nobj, "object_bytes": L, "profile": "clay(20,7,16)",
                        "parallelism": f"objects partitioned over {world} GPU(s)"},
@@ -577,7 +587,7 @@ def copy_inclusive_commit(args, torch, dist, world, slicer, batch, d_in, d_out, 
                 sw.wait(t - 4)
         sw.wait(t)
 
-    for wobj in (64, 128):
+    for wobj in (64, 128, 256):
         if wobj > m:
             continue
         run_stream(wobj)  # warm-up (buffers)

@@ -270,8 +270,9 @@ int te_encode_commit_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint
  * on in order through FuturesOrdered) as one GPU pipeline per handle.
  *   te_stream_writer_new: over ncoders device-bound handles (one per GPU); window t goes to handle
  *     (t - 1) mod ncoders.  Hashing groups of at most group_bytes (input + output; 0 = 1 GiB),
- *     three resident per handle.  The writer owns its streams and device buffers; the handles must
- *     outlive it and must not be re-bound to another device meanwhile.
+ *     three resident per handle.  The writer owns its device buffers and runs on the handles'
+ *     own streams; the handles must outlive it and must not be re-bound to another device
+ *     meanwhile.
  *   te_stream_submit: enqueue one window -- te_encode_commit_batch_host's outputs for its objects
  *     (slices at h_out + out_off, leaf hashes, roots, proofs if h_proofs is not NULL) -- and return
  *     its ticket (1, 2, ... in submission order) without waiting for the device: window t+1's

@@ -167,17 +167,19 @@ struct ClayHost {
                 pos[d0 * q + d1] = (int)order.size();
                 order.push_back(d0 * q + d1);
             }
-        // values: (kind 0 = C / 1 = U, node, plane) -> producer / consumer step
+        // values: (kind 0 = C / 1 = U, node, plane) -> producer / consumer step (flat index: this
+        // runs once per new pattern on the decode path, where random survivor sets are the norm)
         struct Val { int prod = -1, cons = -1; uint32_t loc = kLocNone; };
-        std::map<std::tuple<int, int, int>, int> vid;
+        std::vector<int> vid((size_t)2 * qt * alpha, -1);
         std::vector<Val> vals;
+        vals.reserve(512);
         auto val = [&](int kind, int node, int z) {
-            auto key = std::make_tuple(kind, node, z);
-            auto f = vid.find(key);
-            if (f != vid.end()) return f->second;
-            vid[key] = (int)vals.size();
-            vals.push_back(Val{});
-            return (int)vals.size() - 1;
+            int &id = vid[((size_t)kind * qt + node) * alpha + z];
+            if (id < 0) {
+                id = (int)vals.size();
+                vals.push_back(Val{});
+            }
+            return id;
         };
         struct Ref { int val = -1; };  // value reference to patch with its location
         out.assign(alpha, DecStep{});
@@ -255,22 +257,44 @@ struct ClayHost {
             idx[i] = (int)i;
         }
         std::sort(idx.begin(), idx.end(), [&](int a, int b) { return vals[a].prod < vals[b].prod; });
-        std::vector<int> slot_free, scr_free;  // per location: first step it may be written again
+        // first fit (the lowest free location), linear: producers come in step order, so a
+        // location is released when the producers pass its occupant's consumer step -- per step a
+        // list of the locations it frees, and the free ones as a bit set (this runs once per new
+        // pattern; random survivor sets make that once per stripe)
+        struct Alloc {
+            uint64_t avail[8] = {};   // locations < 512 (the kernels index < 256)
+            int n = 0, next_rel = 0;
+            std::vector<int> head, link;  // per step: first location it frees; per location: next
+            explicit Alloc(int steps) : head((size_t)steps + 1, -1) {}
+            int take(int prod, int cons) {
+                for (; next_rel <= prod; next_rel++)
+                    for (int l = head[(size_t)next_rel]; l >= 0; l = link[(size_t)l])
+                        if (l < 512) avail[l >> 6] |= 1ull << (l & 63);
+                int l = -1;
+                for (int w = 0; w < 8 && l < 0; w++)
+                    if (avail[w]) l = w * 64 + __builtin_ctzll(avail[w]);
+                if (l < 0) {
+                    l = n++;
+                    link.push_back(-1);
+                } else {
+                    avail[l >> 6] &= ~(1ull << (l & 63));
+                }
+                link[(size_t)l] = head[(size_t)cons];
+                head[(size_t)cons] = l;
+                return l;
+            }
+        } slot_alloc(alpha), scr_alloc(alpha);
         for (int i : idx) {
             Val &V = vals[i];
             const bool same_row = V.prod / q == V.cons / q;
-            std::vector<int> &fl = same_row ? slot_free : scr_free;
-            size_t l = 0;
-            while (l < fl.size() && fl[l] > V.prod) l++;
-            if (l == fl.size()) fl.push_back(0);
-            fl[l] = V.cons;
+            const int l = (same_row ? slot_alloc : scr_alloc).take(V.prod, V.cons);
             V.loc = ((same_row ? kLocSlot : kLocScratch) << 24) | (uint32_t)l;
         }
         for (auto &p : pl) *p.first = vals[p.second].loc;
         H = DecProgHdr{};
         H.nsteps = (uint32_t)alpha;
-        H.nslots = (uint32_t)slot_free.size();
-        H.nscratch = (uint32_t)scr_free.size();
+        H.nslots = (uint32_t)slot_alloc.n;
+        H.nscratch = (uint32_t)scr_alloc.n;
         H.max_out = max_out;
         for (uint32_t j = 0; j < P.nknown; j++) H.knode[j] = P.known[j];
         return true;

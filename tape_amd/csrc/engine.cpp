@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <functional>
 #include <thread>
+#include <atomic>
 #include "../../include/tape_ec.h"
 #include "kernels.hpp"
 #include "sha256.hpp"
@@ -272,6 +273,20 @@ struct te_clay {
         std::vector<DecStepP> steps;   // packed program + 2 blank steps
         int orient = 0;                // the program's row orientation (ClayHost::dec_prog)
     };
+    // Device-resident store of staged decode patterns (GpePattern, DecProgHdr, program) by
+    // cache key: a pattern is uploaded once and serves later calls in place.  Random survivor
+    // sets make nearly every stripe a pattern of its own, and re-uploading ~26 KB per stripe per
+    // call cost more host time than the kernel takes.  Slots are handed out in order; a full store
+    // is emptied after its last reader (`used`) has finished.
+    struct DecStore {
+        static constexpr uint32_t kCap = 8192;
+        static constexpr uint32_t kSteps = kRepQ * kRepQ + 2;  // 100 planes + 2 blank steps
+        DevBuf pats, hdrs, steps, soff;
+        std::unordered_map<uint64_t, uint32_t> slot;
+        uint32_t n = 0;
+        hipEvent_t used = nullptr;
+        bool used_pending = false;
+    } dstore;
     // per-pattern decode kernels built at run time (dec_rtc.cpp); created on first decode
     DecJit *jit = nullptr;
     int jit_mode = -1;                 // te_clay_set_decode_jit; -1 = the environment's default
@@ -313,6 +328,12 @@ static void release_device_state(te_clay *c) {
     c->io_out.release();
     c->rec_blob.release();
     c->rec_slices.release();
+    for (DevBuf *b : {&c->dstore.pats, &c->dstore.hdrs, &c->dstore.steps, &c->dstore.soff}) b->release();
+    c->dstore.slot.clear();
+    c->dstore.n = 0;
+    if (c->dstore.used) (void)hipEventDestroy(c->dstore.used);
+    c->dstore.used = nullptr;
+    c->dstore.used_pending = false;
     if (c->rec_done) (void)hipEventDestroy(c->rec_done);
     c->rec_done = nullptr;
     dec_jit_free(c->jit);  // joins compiles in flight; every stream is drained above
@@ -808,15 +829,11 @@ int decode_validate(const te_clay *c, const uint8_t *meta48, uint64_t slice_len,
 }
 
 // The compiled form of one padded erasure pattern, built once per handle (caller holds c->mu).
-// out_node >= 0: the program outputs that internal node's chunk (ClayHost::dec_prog).
-const te_clay::DecCache *dec_pattern(te_clay *c, uint64_t emask, int out_node = -1) {
-    const uint64_t key = emask | (uint64_t)(out_node + 1) << 48;
-    auto f = c->dec_cache.find(key);
-    if (f != c->dec_cache.end()) return &f->second;
-    const ClayHost &h = c->h;
+// Compile one padded erasure pattern (host only, thread-safe: pure ClayHost work).  out_node >= 0:
+// the program outputs that internal node's chunk (ClayHost::dec_prog).
+bool compile_pattern(const ClayHost &h, uint64_t emask, int out_node, te_clay::DecCache &d) {
     const int n = h.n;
-    te_clay::DecCache d;
-    if (!h.gpe_pattern(emask, d.P, d.planes)) return nullptr;
+    if (!h.gpe_pattern(emask, d.P, d.planes)) return false;
     d.P.planes_off = 0;
     // staged kernel (decode_stage.hip): compiled per k with every other node erased (padded
     // patterns); of the two row orientations, two workgroups per CU first (2 x 53 x 1536 B <=
@@ -845,10 +862,104 @@ const te_clay::DecCache *dec_pattern(te_clay *c, uint64_t emask, int out_node = 
             ok = ok && ClayHost::dec_pack(S, d.steps.back());
         }
         d.steps.resize(d.steps.size() + 2);  // blank steps: the kernel reads two steps ahead
-        d.staged = ok;
+        d.staged = ok && d.steps.size() == te_clay::DecStore::kSteps;
         d.H = best;
     }
+    return true;
+}
+
+inline uint64_t dec_key(uint64_t emask, int out_node) { return emask | (uint64_t)(out_node + 1) << 48; }
+
+// The compiled form of one padded erasure pattern, built once per handle (caller holds c->mu).
+const te_clay::DecCache *dec_pattern(te_clay *c, uint64_t emask, int out_node = -1) {
+    const uint64_t key = dec_key(emask, out_node);
+    auto f = c->dec_cache.find(key);
+    if (f != c->dec_cache.end()) return &f->second;
+    te_clay::DecCache d;
+    if (!compile_pattern(c->h, emask, out_node, d)) return nullptr;
     return &c->dec_cache.emplace(key, std::move(d)).first->second;
+}
+
+// Compile the patterns of `keys` missing from the cache, on up to 16 host threads (random
+// survivor sets bring one new pattern per stripe: ~150 us of host work each).
+void dec_precompile(te_clay *c, const std::vector<std::pair<uint64_t, int>> &keys) {
+    std::vector<std::pair<uint64_t, int>> todo;
+    for (const auto &k : keys)
+        if (!c->dec_cache.count(dec_key(k.first, k.second))) todo.push_back(k);
+    if (todo.size() < 8) return;  // dec_pattern compiles the few inline
+    std::vector<te_clay::DecCache> out(todo.size());
+    std::vector<char> ok(todo.size(), 0);
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t nth = std::min<size_t>({16, (size_t)hw, (todo.size() + 7) / 8});
+    std::atomic<size_t> next{0};
+    auto work = [&] {
+        for (size_t i; (i = next.fetch_add(1)) < todo.size();)
+            ok[i] = compile_pattern(c->h, todo[i].first, todo[i].second, out[i]);
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nth; t++) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+    for (size_t i = 0; i < todo.size(); i++)
+        if (ok[i]) c->dec_cache.emplace(dec_key(todo[i].first, todo[i].second), std::move(out[i]));
+}
+
+// Slots of the device-resident pattern store (te_clay::DecStore) for the staged patterns of one
+// call, uploading the ones not there yet.  false: more distinct patterns than the store holds
+// (the call then uploads its patterns through the arena).
+bool dec_store_slots(te_clay *c, const std::vector<const te_clay::DecCache *> &cached, const std::vector<uint64_t> &keys,
+                     std::vector<uint32_t> &slot_of, int &rc) {
+    te_clay::DecStore &S = c->dstore;
+    constexpr uint32_t kCap = te_clay::DecStore::kCap, kSteps = te_clay::DecStore::kSteps;
+    rc = TE_OK;
+    if (keys.size() > kCap) return false;
+    if (!S.pats.p) {
+        if ((rc = hip_status(S.pats.ensure((size_t)kCap * sizeof(GpePattern))))) return false;
+        if ((rc = hip_status(S.hdrs.ensure((size_t)kCap * sizeof(DecProgHdr))))) return false;
+        if ((rc = hip_status(S.steps.ensure((size_t)kCap * kSteps * sizeof(DecStepP))))) return false;
+        if ((rc = hip_status(S.soff.ensure((size_t)kCap * sizeof(uint32_t))))) return false;
+        std::vector<uint32_t> so(kCap);
+        for (uint32_t i = 0; i < kCap; i++) so[i] = i * kSteps;
+        if ((rc = hip_status(hipMemcpy(S.soff.p, so.data(), so.size() * sizeof(uint32_t), hipMemcpyHostToDevice)))) return false;
+        if ((rc = hip_status(hipEventCreateWithFlags(&S.used, hipEventDisableTiming)))) return false;
+        S.slot.clear();
+        S.n = 0;
+    }
+    size_t fresh = 0;
+    for (uint64_t k : keys) fresh += S.slot.count(k) == 0;
+    if (S.n + fresh > kCap) {  // full: empty it once its last reader is done
+        if (S.used_pending && (rc = hip_status(hipEventSynchronize(S.used)))) return false;
+        S.slot.clear();
+        S.n = 0;
+    }
+    slot_of.assign(keys.size(), 0);
+    const uint32_t n0 = S.n;
+    std::vector<GpePattern> np;
+    std::vector<DecProgHdr> nh;
+    std::vector<DecStepP> ns;
+    for (size_t i = 0; i < keys.size(); i++) {
+        auto f = S.slot.find(keys[i]);
+        if (f != S.slot.end()) {
+            slot_of[i] = f->second;
+            continue;
+        }
+        const uint32_t sl = S.n++;
+        S.slot.emplace(keys[i], sl);
+        slot_of[i] = sl;
+        np.push_back(cached[i]->P);
+        nh.push_back(cached[i]->H);
+        ns.insert(ns.end(), cached[i]->steps.begin(), cached[i]->steps.end());
+    }
+    if (!np.empty()) {  // new slots are [n0, n): three copies (synchronous: cold patterns only)
+        if ((rc = hip_status(hipMemcpy(S.pats.as<GpePattern>() + n0, np.data(), np.size() * sizeof(GpePattern),
+                                       hipMemcpyHostToDevice))) ||
+            (rc = hip_status(hipMemcpy(S.hdrs.as<DecProgHdr>() + n0, nh.data(), nh.size() * sizeof(DecProgHdr),
+                                       hipMemcpyHostToDevice))) ||
+            (rc = hip_status(hipMemcpy(S.steps.as<DecStepP>() + (size_t)n0 * kSteps, ns.data(), ns.size() * sizeof(DecStepP),
+                                       hipMemcpyHostToDevice))))
+            return false;
+    }
+    return true;
 }
 
 // Items with lost >= 0 (node recover) need the staged kernel: TE_ERR_UNSUPPORTED, before anything
@@ -858,10 +969,32 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     const ClayHost &h = c->h;
     const int n = h.n;
     const int rotated = (cfg && !raw) ? cfg->rotated : 0;
-    if (c->dec_cache.size() > 1024) c->dec_cache.clear();  // <= ~27 MB (26 KB per pattern; 77,520 masks exist for k = 7)
-    std::map<uint64_t, uint32_t> pat_index;  // erased mask (| output node << 48) -> pattern id
+    // <= ~215 MB of host memory (26 KB per pattern; 77,520 masks exist for k = 7, x 20 outputs
+    // for node recover)
+    if (c->dec_cache.size() > te_clay::DecStore::kCap) c->dec_cache.clear();
+    {
+        std::vector<std::pair<uint64_t, int>> keys;
+        std::unordered_map<uint64_t, char> seen;
+        for (size_t i = 0; i < nitems; i++) {
+            const DecItem &it = items[i];
+            for (uint64_t st = 0; st < it.ns; st++) {
+                uint64_t emask = 0;
+                for (int sh = 0; sh < n; sh++) {
+                    const uint32_t sl = te_shard_to_slice(rotated, (uint32_t)n, (uint32_t)st, (uint32_t)sh);
+                    if (!((it.avail >> sl) & 1u)) emask |= 1ull << h.ext_to_int(sh);
+                }
+                emask = h.pad_erasures(emask);
+                const int onode = it.lost >= 0 ? h.ext_to_int((int)te_slice_to_shard(rotated, (uint32_t)n, (uint32_t)st,
+                                                                                      (uint32_t)it.lost)) : -1;
+                if (seen.emplace(dec_key(emask, onode), 1).second) keys.push_back({emask, onode});
+            }
+        }
+        dec_precompile(c, keys);
+    }
+    std::unordered_map<uint64_t, uint32_t> pat_index;  // erased mask (| output node << 48) -> pattern id
+    std::vector<uint64_t> pat_keys;                    // by pattern id
     bool fused = false;
-    std::vector<GpePattern> pats;
+    std::vector<GpePattern> pats;  // the generic kernel's per-call copies (built only for it)
     std::vector<const te_clay::DecCache *> cached;
     std::vector<uint16_t> pool;
     std::map<uint64_t, std::vector<GpeJob>> groups;  // by chunk size
@@ -885,12 +1018,10 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
             if (f == pat_index.end()) {
                 const te_clay::DecCache *dc = dec_pattern(c, emask, onode);
                 if (!dc) return TE_ERR_BAD_ENCODING;
-                pid = (uint32_t)pats.size();
-                pats.push_back(dc->P);
-                pats.back().planes_off = (uint32_t)pool.size();
-                pool.insert(pool.end(), dc->planes.begin(), dc->planes.end());
+                pid = (uint32_t)cached.size();
                 cached.push_back(dc);
                 pat_index[pkey] = pid;
+                pat_keys.push_back(pkey);
                 max_er = std::max(max_er, dc->P.nerased);
             } else {
                 pid = f->second;
@@ -915,18 +1046,12 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     if (groups.empty()) return TE_OK;
     // staged kernel (decode_stage.hip) when every pattern compiles to a plane program; of the two
     // row orientations the one with fewer scratch rows
-    std::vector<DecProgHdr> dhdrs(pats.size());
-    std::vector<DecStepP> dsteps;
-    std::vector<uint32_t> dstep_off(pats.size());
     uint32_t lds_rows = 0, nscr_max = 0;
     bool staged = true;
-    for (size_t i = 0; i < pats.size() && staged; i++) {
+    for (size_t i = 0; i < cached.size() && staged; i++) {
         const te_clay::DecCache &dc = *cached[i];
         staged = dc.staged;
         if (!staged) break;
-        dhdrs[i] = dc.H;
-        dstep_off[i] = (uint32_t)dsteps.size();
-        dsteps.insert(dsteps.end(), dc.steps.begin(), dc.steps.end());
         lds_rows = std::max(lds_rows, decode_stage_rows(dc.H.nslots, dc.H.max_out));
         nscr_max = std::max(nscr_max, dc.H.nscratch);
     }
@@ -956,10 +1081,10 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
             if (!staged_group(kv.first)) continue;
             const uint32_t sc = (uint32_t)((kv.first >> 32) / (uint64_t)h.alpha);
             const DecJitGeom geo = dec_jit_geom(sc);
-            std::vector<uint64_t> cnt(pats.size(), 0);
+            std::vector<uint64_t> cnt(cached.size(), 0);
             for (const GpeJob &g : kv.second) cnt[g.pattern]++;
-            std::vector<int> fx(pats.size(), -1);
-            for (size_t p = 0; p < pats.size(); p++) {
+            std::vector<int> fx(cached.size(), -1);
+            for (size_t p = 0; p < cached.size(); p++) {
                 // a pattern kernel gets a launch of its own: only worth it for a group that fills
                 // the GPU; smaller groups stay in the shared table-driven launch (recover's
                 // windows hold ~64 stripes per pattern: 80 small launches per step ran 29.3 ms
@@ -979,12 +1104,42 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
             kv.second.swap(rest);
         }
     }
+    // staged patterns live in the device store (uploaded once per handle), the jobs name slots;
+    // otherwise (generic kernel, or more patterns than the store holds) they go in the arena
+    std::vector<uint32_t> slot_of;
+    bool in_store = false;
+    bool every_group_staged = staged;  // the generic kernel reads per-call patterns (plane lists)
+    for (auto &kv : groups) every_group_staged = every_group_staged && (kv.second.empty() || staged_group(kv.first));
+    if (every_group_staged) {
+        int rs = TE_OK;
+        in_store = dec_store_slots(c, cached, pat_keys, slot_of, rs);
+        if (rs) return rs;
+        if (in_store)
+            for (auto &kv : groups)
+                for (GpeJob &g : kv.second) g.pattern = slot_of[g.pattern];
+    }
+    std::vector<DecProgHdr> dhdrs;
+    std::vector<DecStepP> dsteps;
+    std::vector<uint32_t> dstep_off;
+    if (staged && !in_store) {
+        for (size_t i = 0; i < cached.size(); i++) {
+            dhdrs.push_back(cached[i]->H);
+            dstep_off.push_back((uint32_t)dsteps.size());
+            dsteps.insert(dsteps.end(), cached[i]->steps.begin(), cached[i]->steps.end());
+        }
+    }
+    if (!in_store)
+        for (const te_clay::DecCache *dc : cached) {
+            pats.push_back(dc->P);
+            pats.back().planes_off = (uint32_t)pool.size();
+            pool.insert(pool.end(), dc->planes.begin(), dc->planes.end());
+        }
     Arena &A = c->dec;
     A.img.clear();
-    const size_t pat_off = A.put(pats.data(), pats.size() * sizeof(GpePattern));
+    const size_t pat_off = in_store ? 0 : A.put(pats.data(), pats.size() * sizeof(GpePattern));
     const size_t pool_off = A.put(pool.data(), pool.size() * sizeof(uint16_t));
     size_t hdr_off = 0, step_off = 0, soff_off = 0;
-    if (staged) {
+    if (staged && !in_store) {
         hdr_off = A.put(dhdrs.data(), dhdrs.size() * sizeof(DecProgHdr));
         step_off = A.put(dsteps.data(), dsteps.size() * sizeof(DecStepP), 64);
         soff_off = A.put(dstep_off.data(), dstep_off.size() * sizeof(uint32_t));
@@ -1000,10 +1155,17 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         const uint32_t sc = (uint32_t)(cs / (uint64_t)h.alpha);
         DecArgs a{};
         a.jobs = A.at<GpeJob>(o.second);
-        a.patterns = A.at<GpePattern>(pat_off);
-        a.hdrs = A.at<DecProgHdr>(hdr_off);
-        a.steps = A.at<DecStepP>(step_off);
-        a.step_off = A.at<uint32_t>(soff_off);
+        if (in_store) {
+            a.patterns = c->dstore.pats.as<GpePattern>();
+            a.hdrs = c->dstore.hdrs.as<DecProgHdr>();
+            a.steps = c->dstore.steps.as<DecStepP>();
+            a.step_off = c->dstore.soff.as<uint32_t>();
+        } else {
+            a.patterns = A.at<GpePattern>(pat_off);
+            a.hdrs = A.at<DecProgHdr>(hdr_off);
+            a.steps = A.at<DecStepP>(step_off);
+            a.step_off = A.at<uint32_t>(soff_off);
+        }
         a.njobs = (uint32_t)groups[o.first].size();
         a.words_per_stripe = (sc + 3) / 4;
         a.cs = (uint32_t)cs; a.sc = sc; a.n = (uint32_t)n; a.nk = (uint32_t)h.k;
@@ -1076,6 +1238,10 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         TE_HIP(launch_gpe(a, max_er, s));
     }
     kt.stop();
+    if (in_store) {  // a later call that empties the store waits for these launches
+        TE_HIP(hipEventRecord(c->dstore.used, s));
+        c->dstore.used_pending = true;
+    }
     return A.mark_done(s);
 }
 
@@ -1705,10 +1871,7 @@ void writer_release(te_stream_writer::Dev &d) {
     for (auto &b : d.gout) b.release();
     for (auto &b : d.gcom) b.release();
     for (auto &a : d.arena) a.release();
-    d.P.destroy_events();
-    for (auto &s : d.ss)
-        if (s) (void)hipStreamDestroy(s), s = nullptr;
-    if (d.hs) (void)hipStreamDestroy(d.hs), d.hs = nullptr;
+    d.P.destroy_events();  // the streams are the handle's (released with it)
 }
 }  // namespace
 
@@ -1767,9 +1930,19 @@ int te_stream_writer_new(te_clay *const *coders, size_t ncoders, const te_slicer
         d->device = coders[i]->device;
         DeviceGuard dg(d->device);
         if ((rc = hip_status(dg.err))) break;
-        for (int k = 0; k < CommitPipe::S && !rc; k++)
-            rc = hip_status(hipStreamCreateWithFlags(&d->ss[k], hipStreamNonBlocking));
-        if (!rc) rc = hip_status(hipStreamCreateWithFlags(&d->hs, hipStreamNonBlocking));
+        {
+            // the handle's own slot and hashing streams (created if missing): the process has four
+            // hardware queues, and streams of their own would put the writer's slot and hashing
+            // streams on shared queues behind other streams' work (te_encode_commit_batch_host's
+            // note); calls on the handle serialise with the writer's windows on them
+            te_clay *c = coders[i];
+            std::lock_guard<std::mutex> lk(c->mu);
+            for (int k = 0; k < CommitPipe::S && !rc; k++)
+                if (!c->pipe[k].s) rc = hip_status(hipStreamCreateWithFlags(&c->pipe[k].s, hipStreamNonBlocking));
+            if (!rc && !c->stream) rc = hip_status(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+            for (int k = 0; k < CommitPipe::S; k++) d->ss[k] = c->pipe[k].s;
+            d->hs = c->stream;
+        }
         CommitPipe &P = d->P;
         P.hs = d->hs;
         for (int k = 0; k < CommitPipe::S; k++) {

@@ -31,7 +31,7 @@
 #include "dev_io.hpp"
 
 #ifndef TEC_RFOLD_WPE
-#define TEC_RFOLD_WPE 2  // launch bound: minimum waves per SIMD (register budget)
+#define TEC_RFOLD_WPE 4  // 128 VGPRs (52 B/lane spill): 0.567 ms vs 0.63 at 141 VGPRs (1024 x 4 MiB)
 #endif
 #ifndef TEC_RFOLD_ST_AUX
 #define TEC_RFOLD_ST_AUX 2  // cache policy of the lost-chunk row stores (nt)
@@ -198,14 +198,17 @@ __device__ __forceinline__ void rep_fold_body(const RepArgs &a) {
     const uint32_t r_beg = (wv * kQ) / G, r_end = ((wv + 1) * kQ) / G;
 
     // the 10 lost-chunk planes plane p finishes: staged in buffer p & 1, stored whole per row
-    auto finish = [&](uint32_t p, const uint32_t *acc, const uint32_t *ccm) {
-        uint8_t *const stg = lds8 + (p & 1u) * kQ * RS;
+    // the staging buffer alternates with the STEP, not the plane: with a plane of the known set
+    // missing, two consecutive steps can have planes of equal parity (a shared buffer would be
+    // refilled while other waves still store it)
+    auto finish = [&](uint32_t p, uint32_t step, const uint32_t *acc, const uint32_t *ccm) {
+        uint8_t *const stg = lds8 + (step & 1u) * kQ * RS;
 #pragma unroll
         for (int x = 0; x < kQ; x++) {
             const uint32_t v = (uint32_t)x == xl ? acc[x] : lost_c(ccm[x], acc[x]);
             *reinterpret_cast<uint32_t *>(stg + x * RS + col_local) = __builtin_amdgcn_alignbyte(v, v, vsh);
         }
-        lds_barrier();  // staged; buffer (p + 1) & 1 was flushed before this barrier
+        lds_barrier();  // staged; buffer (step + 1) & 1 was flushed before this barrier
         for (uint32_t r = r_beg; r < r_end; r++) {
             const uint8_t *row = stg + r * RS;
             const uint32_t plane = YL == 0 ? r * kQ + p : p * kQ + r;
@@ -254,7 +257,7 @@ __device__ __forceinline__ void rep_fold_body(const RepArgs &a) {
         mds<YL, KM, kQ + kA>(u, acc);
 #pragma unroll
         for (int i = 0; i < kA; i++) *ua_at(i, jp) = acc[kQ + i];
-        finish(p, acc, ccm);
+        finish(p, (uint32_t)jp, acc, ccm);
     }
 #pragma unroll
     for (int ip = 0; ip < kA; ip++) {  // aloof planes: partner aloof node p, U from the known planes
@@ -267,7 +270,7 @@ __device__ __forceinline__ void rep_fold_body(const RepArgs &a) {
         for (int x = 0; x < kQ; x++) ccm[x] = cm[x];
         if (ip + 1 < kA) load_plane((uint32_t)KS.al[ip + 1]);
         mds<YL, KM, kQ>(u, acc);
-        finish(p, acc, ccm);
+        finish(p, (uint32_t)(kK + ip), acc, ccm);
     }
 }
 
