@@ -42,10 +42,15 @@ impl<'a> StreamWriter<'a> {
             ffi::te_stream_submit(self.raw, p.data.as_ptr(), p.objs.as_ptr(), p.objs.len(), p.out.slices.as_mut_ptr(),
                                   p.out.leaf_hashes.as_mut_ptr(), p.out.roots.as_mut_ptr(), p.out.proofs.as_mut_ptr(), &mut t)
         };
-        self.pending.insert(t, p);
+        // a failed window keeps its ticket: `next` reports it in order (its buffers are no longer
+        // referenced by the device once submit has returned)
+        if t != 0 { self.pending.insert(t, p); }
         encode_status(r)?;
         Ok(t)
     }
+
+    /// Windows submitted and not yet handed back by `next`.
+    pub fn in_flight(&self) -> usize { self.pending.len() }
 
     /// The oldest window, completed (FuturesOrdered::next).
     pub fn next(&mut self) -> Option<Result<crate::EncodedWindow, EncodeError>> {

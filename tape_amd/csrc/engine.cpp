@@ -1994,6 +1994,11 @@ int te_stream_submit(te_stream_writer *w, const uint8_t *h_data, const te_object
         for (size_t x = 0; x + 1 < L.gcut.size() && !rc; x++) rc = commit_group(c, &w->cfg, d.P, B, L, x, false);
         if (!rc) rc = hip_status(hipEventCreateWithFlags(&T.done, hipEventDisableTiming));
         if (!rc) rc = hip_status(hipEventRecord(T.done, d.hs));  // after the window's hashing and copies
+        if (rc) {  // groups already enqueued may still read or write the window's host buffers
+            (void)writer_drain(d);
+            if (T.done) (void)hipEventDestroy(T.done);
+            T.done = nullptr;
+        }
     }
     T.rc = rc;
     return rc;
