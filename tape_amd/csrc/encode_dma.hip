@@ -47,6 +47,10 @@ constexpr uint32_t kStageBase = 2 * kSlotBytes;
 constexpr uint32_t kStageRows = TEC_DMA_STAGE_ROWS;  // < 24: timing builds only
 constexpr uint32_t kLdsBytes = kStageBase + kStageRows * RW;
 static_assert(kLdsBytes <= 81920 - 1024, "two workgroups per CU, with a margin");
+#ifndef TEC_DMA_LDS_PAD
+#define TEC_DMA_LDS_PAD 0  // timing builds only: extra LDS requested (occupancy probes)
+#endif
+constexpr uint32_t kLdsLaunch = kLdsBytes + TEC_DMA_LDS_PAD;
 constexpr int kOwnInstr = 10, kPartInstr = 13, kDmaInstr = kOwnInstr + kPartInstr;
 constexpr int kDmaPerWave = (kDmaInstr + G - 1) / G;  // 4 (wave 5: 3)
 constexpr uint32_t kDrop = 0x80000000u;    // offset past every resource: the range check drops it
@@ -475,12 +479,12 @@ hipError_t launch_encode_dma(bool masked, const EncArgs &a, hipStream_t s) {
     if (!encode_dma_supported((int)a.n, 7, a.sc) || a.njobs > 0x7fffffffu) return hipErrorInvalidValue;
     const void *fn = masked ? reinterpret_cast<const void *>(dma::enc_dma_kernel<true>)
                             : reinterpret_cast<const void *>(dma::enc_dma_kernel<false>);
-    hipError_t e = ensure_dyn_lds(fn, dma::kLdsBytes);
+    hipError_t e = ensure_dyn_lds(fn, dma::kLdsLaunch);
     if (e != hipSuccess) return e;
     if (masked)
-        hipLaunchKernelGGL(dma::enc_dma_kernel<true>, dim3(a.njobs), dim3(dma::G * 64), dma::kLdsBytes, s, a);
+        hipLaunchKernelGGL(dma::enc_dma_kernel<true>, dim3(a.njobs), dim3(dma::G * 64), dma::kLdsLaunch, s, a);
     else
-        hipLaunchKernelGGL(dma::enc_dma_kernel<false>, dim3(a.njobs), dim3(dma::G * 64), dma::kLdsBytes, s, a);
+        hipLaunchKernelGGL(dma::enc_dma_kernel<false>, dim3(a.njobs), dim3(dma::G * 64), dma::kLdsLaunch, s, a);
     return hipGetLastError();
 }
 

@@ -302,7 +302,17 @@ struct te_clay {
         bool prog_ok = false;
         int fold = -1;
     };
-    std::map<std::vector<int>, RepCache> rep_cache;
+    struct RepKey {  // (lost shard, helper shard set): rep_pattern depends on the set only
+        uint64_t helpers;
+        uint32_t lost;
+        bool operator==(const RepKey &o) const { return helpers == o.helpers && lost == o.lost; }
+    };
+    struct RepKeyHash {
+        size_t operator()(const RepKey &k) const {
+            return (size_t)((k.helpers ^ ((uint64_t)k.lost << 56)) * 0x9E3779B97F4A7C15ull >> 7);
+        }
+    };
+    std::unordered_map<RepKey, RepCache, RepKeyHash> rep_cache;  // node-based: entries stay put
     struct Slot {
         hipStream_t s = nullptr;
         Arena arena;
@@ -1258,29 +1268,46 @@ struct RepItem {
 int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, size_t nitems, uint8_t *d_out,
                    hipStream_t s) {
     const ClayHost &h = c->h;
-    std::map<std::vector<int>, uint32_t> pat_index;  // (lost, helpers...) -> pattern id
+    using RepKey = te_clay::RepKey;
+    std::unordered_map<RepKey, uint32_t, te_clay::RepKeyHash> pat_index;  // -> pattern id of this call
     std::vector<RepPattern> pats;
     std::vector<const te_clay::RepCache *> cached;  // entries stay put: the map is trimmed only here
     if (c->rep_cache.size() > 4096) c->rep_cache.clear();
     std::vector<uint16_t> pool, pind;
-    std::map<uint64_t, std::vector<RepJob>> groups;  // by chunk size
+    // jobs by (chunk size, folded kernel or not), in first-seen order; usually one chunk size
+    struct Group { uint64_t cs; std::vector<RepJob> jobs[2]; };
+    std::vector<Group> groups;
     std::vector<MetaJob> metas;
     uint32_t max_er = 0;
+    uint64_t run[64];
+    RepKey last_key{~0ull, ~0u};
+    uint32_t last_pid = 0;
     for (size_t i = 0; i < nitems; i++) {
         const te_repair_plan *p = items[i].plan;
-        std::vector<uint64_t> run(p->n, 0);
+        if (p->n > 64) return TE_ERR_INVALID_ARG;
+        std::fill(run, run + p->n, 0ull);
+        Group *grp = nullptr;
+        for (Group &g : groups)
+            if (g.cs == p->cs) grp = &g;
+        if (!grp) {
+            groups.push_back(Group{p->cs, {}});
+            grp = &groups.back();
+            grp->jobs[0].reserve(nitems * p->ns);
+        }
+        const uint32_t sc = (uint32_t)(p->cs / (uint64_t)h.alpha);
         for (uint32_t st = 0; st < p->ns; st++) {
-            std::vector<int> key;
-            key.push_back((int)p->lost_shard[st]);
-            std::vector<int> hs;
-            for (uint32_t j = 0; j < p->d; j++) hs.push_back((int)p->helper_shard[st * p->d + j]);
-            key.insert(key.end(), hs.begin(), hs.end());
-            auto f = pat_index.find(key);
+            const uint32_t *hsh = p->helper_shard.data() + (size_t)st * p->d;
+            RepKey key{0, p->lost_shard[st]};
+            for (uint32_t j = 0; j < p->d; j++) key.helpers |= 1ull << hsh[j];
             uint32_t pid;
-            if (f == pat_index.end()) {
+            auto f = key == last_key ? pat_index.end() : pat_index.find(key);
+            if (key == last_key) {
+                pid = last_pid;
+            } else if (f == pat_index.end()) {
                 auto cf = c->rep_cache.find(key);
                 if (cf == c->rep_cache.end()) {
                     te_clay::RepCache rc;
+                    const std::vector<int> hs(hsh, hsh + p->d);
                     if (!h.rep_pattern((int)p->lost_shard[st], hs, rc.P, rc.pool, rc.pind)) return TE_ERR_CLAY;
                     if (h.nu == 0 && h.n == 2 * h.q && !g_no_fold_repair)
                         rc.fold = repair_fold_column(h.q, h.t, h.k, rc.P.beta, 8, rc.P.lost, rc.P.erased_mask,
@@ -1301,18 +1328,29 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
             } else {
                 pid = f->second;
             }
+            last_key = key;
+            last_pid = pid;
             RepJob j{};
+            const uint8_t *any = nullptr;
             for (uint32_t hj = 0; hj < p->d; hj++) {
                 const uint32_t sl = p->helper_slice[st * p->d + hj];
-                const uint32_t sh = p->helper_shard[st * p->d + hj];
                 const uint64_t off = items[i].helper_off[sl];
                 if (off == ~0ull) return TE_ERR_MISSING_HELPER;
-                j.helper[h.ext_to_int((int)sh)] = d_helpers + off + run[sl];
+                any = j.helper[h.ext_to_int((int)hsh[hj])] = d_helpers + off + run[sl];
                 run[sl] += (uint64_t)p->beta * p->sc;
             }
             j.out = d_out + items[i].out_off + (uint64_t)st * p->cs;
             j.pattern = pid;
-            groups[p->cs].push_back(j);
+            // stripes whose pattern is one of the folded kernel's helper sets of Clay(20,7,16) (all
+            // 19 others available, or one of the other column's first 7 down) go to that kernel,
+            // the rest to the staged / generic kernel
+            const int fc = sc >= 8 ? cached[pid]->fold : -1;
+            if (fc >= 0) {  // the folded kernel loads every node unconditionally (repair_fold.hip)
+                j.aux = pats[pid].lost % (uint32_t)h.q | (uint32_t)fc << 8;
+                for (int nd = 0; nd < h.qt; nd++)
+                    if (!j.helper[nd]) j.helper[nd] = any;
+            }
+            grp->jobs[fc >= 0 ? 0 : 1].push_back(j);
         }
         if (items[i].meta) {
             MetaJob m{};
@@ -1336,33 +1374,14 @@ int repair_enqueue(te_clay *c, const uint8_t *d_helpers, const RepItem *items, s
     const size_t pool_off = A.put(pool.data(), pool.size() * sizeof(uint16_t));
     const size_t pind_off = A.put(pind.data(), pind.size() * sizeof(uint16_t));
     const size_t meta_off = A.put(metas.data(), metas.size() * sizeof(MetaJob));
-    // stripes whose pattern is one of the folded kernel's helper sets of Clay(20,7,16) (all 19
-    // others available, or one of the other column's first 7 down) go to that kernel (one launch
-    // per lost column and set), the rest to the staged / generic kernel
-    std::vector<int> fold_col(pats.size(), -1);
-    for (size_t i = 0; i < pats.size(); i++) fold_col[i] = cached[i]->fold;
+    // one launch per chunk size for the folded kernel (every helper set), one for the others
     struct Launch { uint64_t cs; int fold; size_t off, njobs; };
     std::vector<Launch> offs;
-    for (auto &kv : groups) {
-        const uint32_t sc = (uint32_t)(kv.first / (uint64_t)h.alpha);
-        std::vector<RepJob> part[2];  // folded (one launch, every kernel index), the other stripes
-        for (const RepJob &j : kv.second) {
-            const int fc = sc >= 8 ? fold_col[j.pattern] : -1;
-            RepJob jj = j;
-            if (fc >= 0) {  // the folded kernel loads every node unconditionally (repair_fold.hip)
-                jj.aux = pats[j.pattern].lost % (uint32_t)h.q | (uint32_t)fc << 8;
-                const uint8_t *any = nullptr;
-                for (int nd = 0; nd < h.qt && !any; nd++) any = jj.helper[nd];
-                for (int nd = 0; nd < h.qt; nd++)
-                    if (!jj.helper[nd]) jj.helper[nd] = any;
-            }
-            part[fc >= 0 ? 0 : 1].push_back(jj);
-        }
+    for (Group &g : groups)
         for (int f = 0; f < 2; f++)
-            if (!part[f].empty())
-                offs.push_back({kv.first, f == 0 ? 0 : -1, A.put(part[f].data(), part[f].size() * sizeof(RepJob)),
-                                part[f].size()});
-    }
+            if (!g.jobs[f].empty())
+                offs.push_back({g.cs, f == 0 ? 0 : -1, A.put(g.jobs[f].data(), g.jobs[f].size() * sizeof(RepJob)),
+                                g.jobs[f].size()});
     int r = A.upload(s);
     if (r) return r;
     KTimer kt(s);
