@@ -118,5 +118,15 @@ int main() {
     run<4, 9, true, 0, false, 2>("P4 LP2 part9 bar", din, dout, sink, L2);
     run<2, 9, true, 2, false, 2>("P2 LP2 part9 bar nt loads", din, dout, sink, L2);
     run<2, 9, false, 0, false, 2>("P2 LP2 part9 nobar", din, dout, sink, L2);
+    run<1, 0, true, 0, false>("P1 part0 bar (reads once)", din, dout, sink, L2);
+    run<1, 9, false, 0, false>("P1 part9 nobar", din, dout, sink, L2);
+    run<1, 9, true, 0, true>("P1 part9 bar line-grid stores", din, dout, sink, L2);
+    run<5, 0, true, 0, false>("P5 part0 bar", din, dout, sink, L2);
+    run<10, 0, true, 0, false>("P10 part0 bar", din, dout, sink, L2);
+    run<10, 9, true, 0, false>("P10 part9 bar", din, dout, sink, L2);
+    run<10, 0, false, 0, false>("P10 part0 nobar", din, dout, sink, L2);
+    run<10, 0, true, 0, true>("P10 part0 bar line-grid", din, dout, sink, L2);
+    run<1, 0, true, 0, false, 1, 12>("P1 part0 bar 12 waves 1 WG/CU", din, dout, sink, L1);
+    run<10, 0, true, 0, false, 1, 12>("P10 part0 bar 12 waves 1 WG/CU", din, dout, sink, L1);
     return 0;
 }

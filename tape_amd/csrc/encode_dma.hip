@@ -51,8 +51,17 @@ static_assert(kLdsBytes <= 81920 - 1024, "two workgroups per CU, with a margin")
 #define TEC_DMA_LDS_PAD 0  // timing builds only: extra LDS requested (occupancy probes)
 #endif
 constexpr uint32_t kLdsLaunch = kLdsBytes + TEC_DMA_LDS_PAD;
+#ifndef TEC_DMA_LOADER
+#define TEC_DMA_LOADER 1  // 1: a seventh wave issues every DMA; the six compute waves only store
+#endif
 constexpr int kOwnInstr = 10, kPartInstr = 13, kDmaInstr = kOwnInstr + kPartInstr;
-constexpr int kDmaPerWave = (kDmaInstr + G - 1) / G;  // 4 (wave 5: 3)
+constexpr int kDmaWaves = TEC_DMA_LOADER ? 1 : G;   // waves that issue DMA
+constexpr int kDmaPerWave = (kDmaInstr + kDmaWaves - 1) / kDmaWaves;  // 23 (loader) or 4
+constexpr int kWaves = G + (TEC_DMA_LOADER ? 1 : 0);
+// compute waves keep at most this many stores in flight before B1, so every slice row a
+// later DMA reads back (level-2 partners, >= 8 steps later) has landed: <= 3 steps of stores
+constexpr int kCap = 5;  // flush rows per wave per step
+constexpr int kStoreLag = 6 * kCap;
 constexpr uint32_t kDrop = 0x80000000u;    // offset past every resource: the range check drops it
 #ifndef TEC_DMA_PRIO
 #define TEC_DMA_PRIO 0    // wave priority during a plane's compute (s_setprio)
@@ -67,6 +76,12 @@ constexpr uint32_t kDrop = 0x80000000u;    // offset past every resource: the ra
 #define TEC_DMA_ORDER 1   // 1: a step's stores are issued before the next plane's DMA (B1 waits vmcnt(0));
                           // 0: DMA first, B1 waits vmcnt(2) (measured 3 % slower);
                           // 2: DMA first, B1 waits only for it: the previous step's stores stay in flight
+#endif
+#ifndef TEC_DMA_SLP
+#define TEC_DMA_SLP 1     // MDS as the shared-XOR program (mds_slp.inc); 0: row by row (timing builds)
+#endif
+#ifndef TEC_DMA_WPE
+#define TEC_DMA_WPE 4     // waves per SIMD the register budget is cut for (4: <= 128 VGPRs)
 #endif
 #ifndef TEC_DMA_STORE_MASK
 #define TEC_DMA_STORE_MASK 1  // per-job chunk filter (te_recover_batch_device); 0: timing builds only
@@ -111,7 +126,6 @@ constexpr int kSlots = 25;
 // the rows the step finishes, split into contiguous per-wave shares.  Item = source (0x80 | x:
 // ring own row x; else staging row) | node << 8 | target z0 << 16 (0xff: this step's) |
 // target s << 24 (0xff: this step's).
-constexpr int kCap = 5;
 struct FlushTab {
     struct W {
         uint32_t n;
@@ -207,7 +221,7 @@ __device__ __forceinline__ void col1(const uint32_t *u1, uint32_t (&sl)[kSlots],
 
 // MASKED: the stripe's data end is not dword aligned (an object's last stripe only).
 template <bool MASKED>
-__global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
+__global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint8_t *const lds8 = reinterpret_cast<uint8_t *>(lds);
     const uint32_t lds0 = __builtin_amdgcn_groupstaticsize();  // LDS address of the dynamic array
@@ -262,7 +276,7 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
     uint32_t dvo[kDmaPerWave];
 #pragma unroll
     for (int k = 0; k < kDmaPerWave; k++) {
-        const uint32_t i = wv + (uint32_t)(G * k);
+        const uint32_t i = (TEC_DMA_LOADER ? 0u : wv) + (uint32_t)(kDmaWaves * k);
         dvo[k] = kDrop;
         if (i < (uint32_t)kOwnInstr) {
             const uint32_t b = 64u * i + lane, x = b / RB, j = b - x * RB;
@@ -284,7 +298,7 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
         const uint32_t skip = kQ * sc, skip_from = skip * nz0;
 #pragma unroll
         for (int k = 0; k < kDmaPerWave; k++) {
-            const uint32_t i = wv + (uint32_t)(G * k);
+            const uint32_t i = (TEC_DMA_LOADER ? 0u : wv) + (uint32_t)(kDmaWaves * k);
             if (i >= (uint32_t)kDmaInstr || (TEC_DMA_ABLATE & 2)) continue;
             // lanes past the region's last block are masked off (an LDS-DMA lane that is merely
             // range-dropped still writes zeros to its LDS destination)
@@ -322,9 +336,27 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
     // timing builds only: (cu key, start, end) per workgroup into a.scratch
     uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-    issue_dma(0, 0);
-    issue_dma(1, kSlotBytes);
-    asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");  // plane 0 landed (3 <= pieces of plane 1)
+    if constexpr (TEC_DMA_LOADER) {
+        if (wv == (uint32_t)G) {
+            // the loader: every plane's DMA, two planes ahead of the compute; the barriers
+            // mirror the compute waves' B2 / B1 (the ring slot of plane z is free after B1 of z)
+            issue_dma(0, 0);
+            issue_dma(1, kSlotBytes);
+            asm volatile("s_waitcnt vmcnt(23)\n\ts_barrier" ::: "memory");  // plane 0 landed
+            for (uint32_t z = 0; z < (uint32_t)(kQ * kQ); z++) {
+                lds_barrier();                                  // B2
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // plane z + 1 landed
+                lds_barrier();                                  // B1
+                if (z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, (z & 1u) * kSlotBytes);
+            }
+            return;
+        }
+        asm volatile("s_barrier" ::: "memory");
+    } else {
+        issue_dma(0, 0);
+        issue_dma(1, kSlotBytes);
+        asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");  // plane 0 landed (3 <= pieces of plane 1)
+    }
 
     uint8_t *const stg = lds8 + kStageBase + colw;
     uint32_t prev_n = 0;  // ORDER 2: rows this wave stored last step (2 store instructions each)
@@ -353,7 +385,8 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
                 uint32_t u[K];
 #pragma unroll
                 for (int x = 0; x < K; x++) u[x] = (uint32_t)x == z0 ? own[x] : pft3(own[x], part[x]);
-                enc::mds_rows<K, true, (TEC_DMA_ABLATE & 4) != 0>(u, acc);
+                if constexpr (TEC_DMA_SLP && !(TEC_DMA_ABLATE & 4)) enc::mds7_slp<true>(u, acc);
+                else enc::mds_rows<K, true, (TEC_DMA_ABLATE & 4) != 0>(u, acc);
 #pragma unroll
                 for (int r = 0; r < 3; r++)
                     st32(stg + (kRowC0 + r) * RW, acc[r] ^ mulc(kPft.t_p[1], part[K + r]));
@@ -363,7 +396,8 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
                 uint32_t u[K];
 #pragma unroll
                 for (int x = 0; x < K; x++) u[x] = pft3(own[x], part[x]);
-                enc::mds_rows<K, false, (TEC_DMA_ABLATE & 4) != 0>(u, acc);
+                if constexpr (TEC_DMA_SLP && !(TEC_DMA_ABLATE & 4)) enc::mds7_slp<false>(u, acc);
+                else enc::mds_rows<K, false, (TEC_DMA_ABLATE & 4) != 0>(u, acc);
                 const uint32_t i0 = z0 - K;
 #pragma unroll
                 for (int r = 0; r < 3; r++) {
@@ -413,7 +447,10 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
             }
             // B1: the next plane's DMA has landed (this wave's pieces are older than its last
             // step's >= 2 stores) and every wave is done reading this slot and the staging rows
-            if constexpr (!(TEC_DMA_ABLATE & 8)) {
+            if constexpr (TEC_DMA_LOADER) {
+                // no loads to wait for: only bound the stores in flight (see kStoreLag)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kStoreLag) : "memory");
+            } else if constexpr (!(TEC_DMA_ABLATE & 8)) {
                 if constexpr (TEC_DMA_ORDER == 2) {
                     // outstanding, oldest first: the next plane's DMA pieces, then the previous
                     // step's 2 x prev_n stores -- wait for the DMA only
@@ -432,7 +469,7 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
                 }
             }
             lds_barrier();
-            if (TEC_DMA_ORDER != 1 && z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, slot);
+            if (!TEC_DMA_LOADER && TEC_DMA_ORDER != 1 && z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, slot);
             prev_n = (TEC_DMA_ABLATE & 1) ? 0u : n;
 #pragma unroll
             for (int q = 0; q < kCap; q++) {
@@ -441,7 +478,7 @@ __global__ void __launch_bounds__(G * 64, 4) enc_dma_kernel(EncArgs a) {
                     __builtin_amdgcn_raw_buffer_store_b128(d1[q], rb_dst, (int)vo1, (int)dst[q], TEC_DMA_ST_AUX);
                 }
             }
-            if (TEC_DMA_ORDER == 1 && z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, slot);
+            if (!TEC_DMA_LOADER && TEC_DMA_ORDER == 1 && z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, slot);
         }
     }
     // the last plane's left-over row (its staging row is untouched since the last compute)
@@ -482,9 +519,9 @@ hipError_t launch_encode_dma(bool masked, const EncArgs &a, hipStream_t s) {
     hipError_t e = ensure_dyn_lds(fn, dma::kLdsLaunch);
     if (e != hipSuccess) return e;
     if (masked)
-        hipLaunchKernelGGL(dma::enc_dma_kernel<true>, dim3(a.njobs), dim3(dma::G * 64), dma::kLdsLaunch, s, a);
+        hipLaunchKernelGGL(dma::enc_dma_kernel<true>, dim3(a.njobs), dim3(dma::kWaves * 64), dma::kLdsLaunch, s, a);
     else
-        hipLaunchKernelGGL(dma::enc_dma_kernel<false>, dim3(a.njobs), dim3(dma::G * 64), dma::kLdsLaunch, s, a);
+        hipLaunchKernelGGL(dma::enc_dma_kernel<false>, dim3(a.njobs), dim3(dma::kWaves * 64), dma::kLdsLaunch, s, a);
     return hipGetLastError();
 }
 
