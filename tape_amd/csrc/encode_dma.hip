@@ -61,7 +61,11 @@ constexpr int kWaves = G + (TEC_DMA_LOADER ? 1 : 0);
 // compute waves keep at most this many stores in flight before B1, so every slice row a
 // later DMA reads back (level-2 partners, >= 8 steps later) has landed: <= 3 steps of stores
 constexpr int kCap = 5;  // flush rows per wave per step
-constexpr int kStoreLag = 6 * kCap;
+#ifndef TEC_DMA_LAG
+#define TEC_DMA_LAG 30
+#endif
+constexpr int kStoreLag = TEC_DMA_LAG;
+static_assert(kStoreLag <= 3 * 2 * kCap && kStoreLag < 64, "stores older than 3 steps must have landed");
 constexpr uint32_t kDrop = 0x80000000u;    // offset past every resource: the range check drops it
 #ifndef TEC_DMA_PRIO
 #define TEC_DMA_PRIO 0    // wave priority during a plane's compute (s_setprio)

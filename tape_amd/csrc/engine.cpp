@@ -1675,29 +1675,60 @@ static void commit_plan(const CommitBatch &B, uint64_t group_bytes, uint64_t cop
     }
 }
 
-// Enqueue group x of plan L.  `last`: the caller's final group -- its encodes run ahead of the
-// copies (one D2H per two encodes on a slot, the rest after the group's last encode), so its
-// hashing, the only exposed one, starts about halfway through the group's copies.
-static int commit_group(te_clay *c, const te_slicer_cfg *cfg, CommitPipe &P, const CommitBatch &B,
-                        const CommitPlan &L, size_t x, bool last) {
-    constexpr int R = CommitPipe::R, S = CommitPipe::S;
-    const size_t i = L.gcut[x], j = L.gcut[x + 1], r = P.groups % R;
+// A group's commitment outputs on the device: leaf hashes of row q at q * leaf_b, roots after
+// `rows_cap` rows of leaves, proofs after the roots (rows = objects, in group order).
+struct GroupSeg {
+    CommitOut co;            // the host outputs of the segment's window
+    size_t obj0 = 0;         // first object of the segment in its window (host output index)
+    uint64_t row0 = 0, cnt = 0, gout_off = 0;
+    std::vector<uint64_t> slice_len, out_bytes;
+};
+struct OpenGroup {
+    bool open = false;
+    size_t r = 0;                 // group buffer
+    uint64_t out_off = 0, rows = 0, rows_cap = 0, bytes = 0;
+    bool slots_used[CommitPipe::S] = {};
+    std::vector<GroupSeg> segs;
+};
+
+// Open a group in the next group buffer: its previous group must be hashed (and copied out)
+// before the slot streams write into it.  need_out / need_rows: what the first segment needs
+// (a buffer grows only after the work queued on it has drained).
+static int group_open(CommitPipe &P, OpenGroup &G, uint64_t need_out, uint64_t need_rows, uint64_t row_b) {
+    constexpr int S = CommitPipe::S;
+    const size_t r = P.groups % CommitPipe::R;
+    if (P.gout[r]->cap < need_out || P.gcom[r]->cap < need_rows * row_b) {
+        if (!P.grow_ok) return TE_ERR_INVALID_ARG;
+        if (P.hashed_pending[r]) TE_HIP(hipEventSynchronize(P.ev_hashed[r]));
+        TE_HIP(P.gout[r]->ensure(need_out));
+        TE_HIP(P.gcom[r]->ensure(need_rows * row_b));
+    }
+    if (P.hashed_pending[r])
+        for (int k = 0; k < S; k++) TE_HIP(hipStreamWaitEvent(P.ss[k], P.ev_hashed[r], 0));
+    G.open = true;
+    G.r = r;
+    G.out_off = G.rows = G.bytes = 0;
+    G.rows_cap = row_b ? P.gcom[r]->cap / row_b : 0;
+    for (int k = 0; k < S; k++) G.slots_used[k] = false;
+    G.segs.clear();
+    return TE_OK;
+}
+
+// Encode group x of plan L into the open group (after its earlier segments): H2D, encode and D2H
+// of the slices per copy window, rotating over the slot streams.  `last`: the caller's final group
+// -- its encodes run ahead of the copies (one D2H per two encodes on a slot, the rest after the
+// group's last encode), so its hashing, the only exposed one, starts about halfway through the
+// group's copies.
+static int group_add(te_clay *c, const te_slicer_cfg *cfg, CommitPipe &P, OpenGroup &G, const CommitBatch &B,
+                     const CommitPlan &L, size_t x, bool last) {
+    constexpr int S = CommitPipe::S;
+    const size_t i = L.gcut[x], j = L.gcut[x + 1];
     const std::vector<size_t> &wc = L.wcut[x];
-    uint64_t gout_bytes = 0, win_in_max = 16;
-    for (size_t o = i; o < j; o++) gout_bytes += B.out_bytes[o];
+    uint64_t win_in_max = 16;
     for (size_t y = 0; y + 1 < wc.size(); y++) {
         uint64_t win_in = 16;
         for (size_t o = wc[y]; o < wc[y + 1]; o++) win_in += B.in_bytes(o);
         win_in_max = std::max(win_in_max, win_in);
-    }
-    const uint64_t commit_bytes = (uint64_t)(j - i) * (B.leaf_b + TE_HASH_SIZE + B.proof_b);
-    // buffers: pre-sized by the one-shot path; a stream writer grows one only after the work
-    // queued on it has drained (never under queued work)
-    if (P.gout[r]->cap < gout_bytes || P.gcom[r]->cap < commit_bytes) {
-        if (!P.grow_ok) return TE_ERR_INVALID_ARG;
-        if (P.hashed_pending[r]) TE_HIP(hipEventSynchronize(P.ev_hashed[r]));
-        TE_HIP(P.gout[r]->ensure(gout_bytes));
-        TE_HIP(P.gcom[r]->ensure(commit_bytes));
     }
     for (int k = 0; k < S; k++)
         if (P.in[k]->cap < win_in_max) {
@@ -1705,12 +1736,16 @@ static int commit_group(te_clay *c, const te_slicer_cfg *cfg, CommitPipe &P, con
             TE_HIP(hipStreamSynchronize(P.ss[k]));
             TE_HIP(P.in[k]->ensure(win_in_max));
         }
-    uint8_t *gout = P.gout[r]->as<uint8_t>();
-    if (P.hashed_pending[r])  // the buffer's previous group must be hashed (and, before that, copied out)
-        for (int k = 0; k < S; k++) TE_HIP(hipStreamWaitEvent(P.ss[k], P.ev_hashed[r], 0));
+    GroupSeg seg;
+    seg.co = B.co;
+    seg.obj0 = i;
+    seg.row0 = G.rows;
+    seg.cnt = j - i;
+    seg.gout_off = G.out_off;
+    uint8_t *gout = P.gout[G.r]->as<uint8_t>();
     std::deque<std::vector<CopyRun>> pend[S];
     int encs[S] = {};
-    uint64_t dout = 0;
+    uint64_t dout = G.out_off;
     std::vector<te_object> local;
     std::vector<CopyRun> hin, hout;
     int rc = TE_OK;
@@ -1729,52 +1764,88 @@ static int commit_group(te_clay *c, const te_slicer_cfg *cfg, CommitPipe &P, con
             pend[k].pop_front();
         }
         P.slot_used[k] = true;
+        G.slots_used[k] = true;
         for (size_t o = a; o < b; o++) dout += B.out_bytes[o];
         P.w++;
     }
     for (int k = 0; k < S && !rc; k++) {
         for (; !pend[k].empty() && !rc; pend[k].pop_front())
             rc = copy_runs(pend[k].front(), gout, B.h_out, hipMemcpyDeviceToHost, P.ss[k]);
-        if (!rc && P.slot_used[k]) rc = hip_status(hipEventRecord(P.ev_slot[k], P.ss[k]));
+        if (!rc && G.slots_used[k]) rc = hip_status(hipEventRecord(P.ev_slot[k], P.ss[k]));
     }
     if (rc) return rc;
-    // hashing starts once the group is encoded, not copied out: the last windows' D2H overlaps it
-    // (11.9 -> 12.4-12.6 GiB/s, one box)
+    for (size_t o = i; o < j; o++) {
+        seg.slice_len.push_back(B.slice_len[o]);
+        seg.out_bytes.push_back(B.out_bytes[o]);
+        G.bytes += B.objs[o].blob_len + B.out_bytes[o];
+    }
+    G.out_off = dout;
+    G.rows += seg.cnt;
+    G.segs.push_back(std::move(seg));
+    return TE_OK;
+}
+
+// Hash the open group: once every slot stream has encoded its last window (the last windows' D2H
+// overlaps the hashing: 11.9 -> 12.4-12.6 GiB/s, one box), one leaf/tree launch per run of equal
+// slice lengths across all its segments, then the D2H of each segment's leaf hashes, roots and
+// proofs into its window's host buffers.
+static int group_close(CommitPipe &P, OpenGroup &G, uint32_t n, uint32_t height, uint64_t leaf_b, uint64_t proof_b) {
+    constexpr int S = CommitPipe::S;
+    if (!G.open) return TE_OK;
+    G.open = false;
     for (int k = 0; k < S; k++)
-        if (P.slot_used[k]) TE_HIP(hipStreamWaitEvent(P.hs, P.ev_enc[k], 0));
-    // commitments of the group's objects, one launch per run of equal slice lengths
-    const uint64_t cnt = j - i, root_at = cnt * B.leaf_b, proof_at = root_at + cnt * TE_HASH_SIZE;
-    uint8_t *dc = P.gcom[r]->as<uint8_t>();
-    uint64_t off = 0;
-    for (size_t o = i; o < j;) {
+        if (G.slots_used[k]) TE_HIP(hipStreamWaitEvent(P.hs, P.ev_enc[k], 0));
+    uint8_t *gout = P.gout[G.r]->as<uint8_t>(), *dc = P.gcom[G.r]->as<uint8_t>();
+    const uint64_t root_at = G.rows_cap * leaf_b, proof_at = root_at + G.rows_cap * TE_HASH_SIZE;
+    // flatten the rows: (slice length, out bytes, slice offset) in group order
+    struct Row { uint64_t slen, obytes, off; };
+    std::vector<Row> rows;
+    rows.reserve(G.rows);
+    for (const GroupSeg &sg : G.segs) {
+        uint64_t off = sg.gout_off;
+        for (size_t q = 0; q < sg.cnt; q++) {
+            rows.push_back({sg.slice_len[q], sg.out_bytes[q], off});
+            off += sg.out_bytes[q];
+        }
+    }
+    for (size_t o = 0; o < rows.size();) {
         size_t e = o + 1;
-        while (e < j && B.slice_len[e] == B.slice_len[o]) e++;
+        while (e < rows.size() && rows[e].slen == rows[o].slen) e++;
         CommitArgs ca{};
-        ca.slices = gout + off;
-        ca.obj_stride = B.out_bytes[o];
-        ca.slice_len = B.slice_len[o];
-        ca.n = B.n;
+        ca.slices = gout + rows[o].off;
+        ca.obj_stride = rows[o].obytes;
+        ca.slice_len = rows[o].slen;
+        ca.n = n;
         ca.nobj = (uint32_t)(e - o);
-        ca.height = B.co.height;
-        ca.leaf = dc + (o - i) * B.leaf_b;
-        ca.root = dc + root_at + (o - i) * TE_HASH_SIZE;
-        ca.proof = B.co.proof ? dc + proof_at + (o - i) * B.proof_b : nullptr;
+        ca.height = height;
+        ca.leaf = dc + o * leaf_b;
+        ca.root = dc + root_at + o * TE_HASH_SIZE;
+        ca.proof = proof_b ? dc + proof_at + o * proof_b : nullptr;
         TE_HIP(launch_commit(ca, P.hs));
-        off += (e - o) * B.out_bytes[o];
         o = e;
     }
-    const struct { uint8_t *h; uint64_t d, len; } back[3] = {
-        {B.co.leaf + i * B.leaf_b, 0, cnt * B.leaf_b},
-        {B.co.root + i * TE_HASH_SIZE, root_at, cnt * TE_HASH_SIZE},
-        {B.co.proof ? B.co.proof + i * B.proof_b : nullptr, proof_at, cnt * B.proof_b}};
-    for (const auto &bk : back)
-        if (bk.h && bk.len) TE_HIP(hipMemcpyAsync(bk.h, dc + bk.d, bk.len, hipMemcpyDeviceToHost, P.hs));
+    for (const GroupSeg &sg : G.segs) {
+        const struct { uint8_t *h; uint64_t d, len; } back[3] = {
+            {sg.co.leaf + sg.obj0 * leaf_b, sg.row0 * leaf_b, sg.cnt * leaf_b},
+            {sg.co.root + sg.obj0 * TE_HASH_SIZE, root_at + sg.row0 * TE_HASH_SIZE, sg.cnt * TE_HASH_SIZE},
+            {sg.co.proof ? sg.co.proof + sg.obj0 * proof_b : nullptr, proof_at + sg.row0 * proof_b, sg.cnt * proof_b}};
+        for (const auto &bk : back)
+            if (bk.h && bk.len) TE_HIP(hipMemcpyAsync(bk.h, dc + bk.d, bk.len, hipMemcpyDeviceToHost, P.hs));
+    }
     for (int k = 0; k < S; k++)
-        if (P.slot_used[k]) TE_HIP(hipStreamWaitEvent(P.hs, P.ev_slot[k], 0));
-    TE_HIP(hipEventRecord(P.ev_hashed[r], P.hs));
-    P.hashed_pending[r] = true;
+        if (G.slots_used[k]) TE_HIP(hipStreamWaitEvent(P.hs, P.ev_slot[k], 0));
+    TE_HIP(hipEventRecord(P.ev_hashed[G.r], P.hs));
+    P.hashed_pending[G.r] = true;
     P.groups++;
+    G.segs.clear();
     return TE_OK;
+}
+
+// The bytes a group of plan L needs in a group buffer, and its commitment rows.
+static void group_need(const CommitBatch &B, const CommitPlan &L, size_t x, uint64_t &out, uint64_t &rows) {
+    out = 0;
+    for (size_t o = L.gcut[x]; o < L.gcut[x + 1]; o++) out += B.out_bytes[o];
+    rows = L.gcut[x + 1] - L.gcut[x];
 }
 
 static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data,
@@ -1824,7 +1895,15 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
         TE_HIP(P.gcom[r]->ensure(commit_cap));
     }
     rc = P.make_events();
-    for (size_t x = 0; x < ngroups && rc == TE_OK; x++) rc = commit_group(c, cfg, P, B, L, x, x + 1 == ngroups);
+    const uint64_t row_b = B.leaf_b + TE_HASH_SIZE + B.proof_b;
+    OpenGroup G;
+    for (size_t x = 0; x < ngroups && rc == TE_OK; x++) {
+        uint64_t need_out, need_rows;
+        group_need(B, L, x, need_out, need_rows);
+        rc = group_open(P, G, need_out, need_rows, row_b);
+        if (!rc) rc = group_add(c, cfg, P, G, B, L, x, x + 1 == ngroups);
+        if (!rc) rc = group_close(P, G, B.n, B.co.height, B.leaf_b, B.proof_b);
+    }
     for (auto &sl : c->pipe) {
         const int r2 = hip_status(hipStreamSynchronize(sl.s));
         if (rc == TE_OK) rc = r2;
@@ -1851,11 +1930,17 @@ struct te_stream_writer {
         hipStream_t ss[CommitPipe::S] = {}, hs = nullptr;
         DevBuf in[CommitPipe::S], gout[CommitPipe::R], gcom[CommitPipe::R];
         Arena arena[CommitPipe::S];
+        // windows share a hashing group until it holds group_bytes / 2 (a leaf launch costs one
+        // slice's SHA-256 whatever its size: one launch per window capped small windows at
+        // 7.3-7.5 GiB/s); tickets whose last group is still open complete when it closes
+        OpenGroup G;
+        std::vector<uint64_t> pend;
     };
     struct Ticket {
         int dev = -1;
         hipEvent_t done = nullptr;
         int rc = TE_OK;
+        bool pending = false;  // its last group is the device's open group
     };
     std::vector<std::unique_ptr<Dev>> devs;
     te_slicer_cfg cfg{};
@@ -1868,6 +1953,38 @@ struct te_stream_writer {
 };
 
 namespace {
+uint64_t writer_row_bytes(const te_stream_writer &w, const te_stream_writer::Dev &d, uint64_t &leaf_b, uint64_t &proof_b) {
+    leaf_b = (uint64_t)d.c->h.n * TE_HASH_SIZE;
+    proof_b = leaf_b * w.height;  // proofs always computed (a window may ask for them)
+    return leaf_b + TE_HASH_SIZE + proof_b;
+}
+// Hash the device's open group and complete the tickets waiting on it.  Called with w.mu held.
+int writer_close(te_stream_writer &w, te_stream_writer::Dev &d) {
+    int rc = TE_OK;
+    if (d.G.open) {
+        uint64_t leaf_b, proof_b;
+        (void)writer_row_bytes(w, d, leaf_b, proof_b);
+        std::lock_guard<std::mutex> lk(d.c->mu);
+        DeviceGuard dg(d.device);
+        rc = hip_status(dg.err);
+        if (!rc) rc = group_close(d.P, d.G, (uint32_t)d.c->h.n, w.height, leaf_b, proof_b);
+    }
+    for (uint64_t t : d.pend) {
+        auto it = w.tickets.find(t);
+        if (it == w.tickets.end()) continue;
+        te_stream_writer::Ticket &T = it->second;
+        T.pending = false;
+        if (!rc) {
+            DeviceGuard dg(d.device);
+            rc = hip_status(hipEventCreateWithFlags(&T.done, hipEventDisableTiming));
+            if (!rc) rc = hip_status(hipEventRecord(T.done, d.hs));  // after the group's hashing and copies
+            if (rc && T.done) (void)hipEventDestroy(T.done), T.done = nullptr;
+        }
+        if (rc && !T.rc) T.rc = rc;
+    }
+    d.pend.clear();
+    return rc;
+}
 int writer_drain(te_stream_writer::Dev &d) {
     DeviceGuard dg(d.device);
     TE_HIP(dg.err);
@@ -2007,16 +2124,61 @@ int te_stream_submit(te_stream_writer *w, const uint8_t *h_data, const te_object
         CommitPlan L;
         const uint64_t copy_bytes = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)128 << 20, w->group_bytes / 8));
         commit_plan(B, w->group_bytes, copy_bytes, L);
-        std::lock_guard<std::mutex> lk(c->mu);
-        DeviceGuard dg(d.device);
-        rc = c->device != d.device ? TE_ERR_INVALID_ARG : hip_status(dg.err);  // handle re-bound under the writer
-        for (size_t x = 0; x + 1 < L.gcut.size() && !rc; x++) rc = commit_group(c, &w->cfg, d.P, B, L, x, false);
-        if (!rc) rc = hip_status(hipEventCreateWithFlags(&T.done, hipEventDisableTiming));
-        if (!rc) rc = hip_status(hipEventRecord(T.done, d.hs));  // after the window's hashing and copies
+        uint64_t leaf_b, proof_b;
+        const uint64_t row_b = writer_row_bytes(*w, d, leaf_b, proof_b);
+        B.leaf_b = leaf_b;
+        B.proof_b = proof_b;
+        const uint64_t close_at = std::max<uint64_t>(1, w->group_bytes / 2);
+        for (size_t x = 0; x + 1 < L.gcut.size() && !rc; x++) {
+            uint64_t need_out, need_rows, gbytes = 0;
+            group_need(B, L, x, need_out, need_rows);
+            for (size_t o = L.gcut[x]; o < L.gcut[x + 1]; o++) gbytes += B.objs[o].blob_len + B.out_bytes[o];
+            OpenGroup &G = d.G;
+            if (G.open && (G.out_off + need_out > d.P.gout[G.r]->cap || G.rows + need_rows > G.rows_cap ||
+                           G.bytes + gbytes > w->group_bytes))
+                rc = writer_close(*w, d);  // earlier windows' tickets complete with it
+            if (rc) break;
+            {
+                std::lock_guard<std::mutex> lk(c->mu);
+                DeviceGuard dg(d.device);
+                rc = c->device != d.device ? TE_ERR_INVALID_ARG : hip_status(dg.err);  // handle re-bound under the writer
+                if (!rc && !G.open) {
+                    // a group buffer holds a full group's slices (group_bytes of objects + slices,
+                    // ~3/4 of it slices for Clay(20, 7)) and its commitment rows
+                    const uint64_t want_out = std::max<uint64_t>(need_out, w->group_bytes - w->group_bytes / 4);
+                    const uint64_t want_rows = std::max<uint64_t>(need_rows, 4096);
+                    rc = group_open(d.P, G, want_out, want_rows, row_b);
+                }
+                if (!rc) rc = group_add(c, &w->cfg, d.P, G, B, L, x, false);
+            }
+            if (!rc && G.bytes >= close_at) rc = writer_close(*w, d);  // pending windows complete with it
+        }
+        if (!rc) {
+            if (d.G.open) {
+                T.pending = true;
+                d.pend.push_back(t);
+            } else {
+                // this window's last group is hashed (queued): it and any earlier pending windows
+                // complete after it
+                d.pend.push_back(t);
+                T.pending = true;
+                rc = writer_close(*w, d);
+            }
+        }
         if (rc) {  // groups already enqueued may still read or write the window's host buffers
             (void)writer_drain(d);
+            d.G.open = false;
+            for (uint64_t pt : d.pend) {
+                auto it = w->tickets.find(pt);
+                if (it != w->tickets.end()) {
+                    it->second.pending = false;
+                    if (!it->second.rc) it->second.rc = rc;
+                }
+            }
+            d.pend.clear();
             if (T.done) (void)hipEventDestroy(T.done);
             T.done = nullptr;
+            T.pending = false;
         }
     }
     T.rc = rc;
@@ -2034,6 +2196,11 @@ int te_stream_wait(te_stream_writer *w, uint64_t ticket) {
             if (ticket >= w->next) return TE_ERR_INVALID_ARG;  // never submitted
             if (w->tickets.empty() || w->tickets.begin()->first > ticket) return first;
             t = w->tickets.begin()->first;
+            if (w->tickets.begin()->second.pending) {  // its group is still open: hash it now
+                te_stream_writer::Dev &d = *w->devs[(size_t)w->tickets.begin()->second.dev];
+                const int r = writer_close(*w, d);
+                if (r) (void)writer_drain(d);
+            }
             T = w->tickets.begin()->second;
         }
         int rc = T.rc;
