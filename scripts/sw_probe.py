@@ -11,6 +11,8 @@ from tape_amd import batch
 
 m, L, N, H = 1024, 4 << 20, 20, 5
 gb = int(float(sys.argv[1]) * (1 << 30)) if len(sys.argv) > 1 else 4 << 30
+only = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [32, 64, 128, 256]
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 s = T.Slicer.clay_default()
 per = s.geometry(L).slice_len * N
 h_in = torch.randint(0, 256, (m * L,), dtype=torch.uint8).pin_memory()
@@ -37,10 +39,10 @@ def run(wobj):
     sw.wait(t)
 
 
-for wobj in (32, 64, 128, 256):
+for wobj in only:
     run(wobj)
     r = []
-    for _ in range(3):
+    for _ in range(reps):
         t0 = time.perf_counter()
         run(wobj)
         r.append(round(m * L / (time.perf_counter() - t0) / 2**30, 2))

@@ -16,7 +16,14 @@
 namespace tec {
 namespace commit {
 
-__global__ void __launch_bounds__(64) leaf_kernel(CommitArgs a) {
+constexpr uint64_t kLeafBlocksPerLaunch = 1536;  // ~3.5 ms of one stream's SHA-256
+
+// Blocks [b0, b1) of every stream.  A stream's state between launches lives in its own leaf-hash
+// slot (8 words, the size of the digest): launches after the first load it, launches before the
+// last store it, and the last stores the digest.  Long slices are hashed in several launches of
+// about kLeafBlocksPerLaunch blocks (a 30 ms launch holds up any copy queued behind it
+// on a shared hardware queue; ~3 ms launches do not).
+__global__ void __launch_bounds__(64) leaf_kernel(CommitArgs a, uint64_t b0, uint64_t b1) {
     const uint32_t total = a.nobj * a.n;
     const uint32_t gid = blockIdx.x * 64u + threadIdx.x;
     const bool live = gid < total;
@@ -26,28 +33,44 @@ __global__ void __launch_bounds__(64) leaf_kernel(CommitArgs a) {
     const uint64_t L = a.slice_len, M = L + 4u;       // message bytes ("LEAF" || slice)
     const uint64_t T = (M + 8u) / 64u + 1u;           // blocks incl. padding and length
     const uint64_t nfull = L >= 60u ? (L - 60u) / 64u + 1u : 0u;  // blocks 0 .. nfull-1 hold data only
+    if (b1 > T) b1 = T;
+    uint32_t *out = reinterpret_cast<uint32_t *>(a.leaf + (uint64_t)g * 32u);
     uint32_t st[8];
-    sha::init(st);
-    // raw (little-endian) words of the next block, loaded one block ahead and byte-swapped only
-    // when that block starts, so the loads' latency hides behind a whole compression
-    uint32_t w[16], nx[16];
-    if (nfull) {
-        nx[0] = sha::bswap(sha::kLeafWord);
+    if (b0 == 0) {
+        sha::init(st);
+    } else {
 #pragma unroll
-        for (int k = 1; k < 16; k++) nx[k] = p[k - 1];
+        for (int i = 0; i < 8; i++) st[i] = out[i];
     }
-    for (uint64_t b = 0; b < nfull; b++) {
+    // raw (little-endian) words of the next two blocks, loaded two blocks ahead and byte-swapped
+    // only when their block starts, so a load's latency hides behind two compressions (the hashing
+    // runs beside copies and encodes, whose traffic lengthens it)
+    uint32_t w[16], n1[16], n2[16];
+    const uint64_t dend = nfull < b1 ? nfull : b1;
+    auto ldblk = [&](uint64_t b, uint32_t *dst) {
+        if (b == 0) {
+            dst[0] = sha::bswap(sha::kLeafWord);
 #pragma unroll
-        for (int k = 0; k < 16; k++) w[k] = sha::bswap(nx[k]);
-        if (b + 1 < nfull) {
-            const uint32_t *q = p + (b + 1) * 16u - 1u;
+            for (int k = 1; k < 16; k++) dst[k] = p[k - 1];
+        } else {
+            const uint32_t *q = p + b * 16u - 1u;
 #pragma unroll
-            for (int k = 0; k < 16; k++) nx[k] = q[k];
+            for (int k = 0; k < 16; k++) dst[k] = q[k];
         }
+    };
+    if (b0 < dend) ldblk(b0, n1);
+    if (b0 + 1 < dend) ldblk(b0 + 1, n2);
+    for (uint64_t b = b0; b < dend; b++) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            w[k] = sha::bswap(n1[k]);
+            n1[k] = n2[k];
+        }
+        if (b + 2 < dend) ldblk(b + 2, n2);
         sha::compress(st, w);
     }
     // the last data bytes, the 0x80 terminator, zeros and the bit length (L % 4 == 0)
-    for (uint64_t b = nfull; b < T; b++) {
+    for (uint64_t b = (nfull > b0 ? nfull : b0); b < b1; b++) {
 #pragma unroll
         for (int k = 0; k < 16; k++) {
             const uint64_t gw = b * 16u + (uint64_t)k, pos = gw * 4u;
@@ -60,9 +83,13 @@ __global__ void __launch_bounds__(64) leaf_kernel(CommitArgs a) {
         sha::compress(st, w);
     }
     if (!live) return;
-    uint32_t *out = reinterpret_cast<uint32_t *>(a.leaf + (uint64_t)gid * 32u);
+    if (b1 < T) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) out[i] = sha::bswap(st[i]);
+        for (int i = 0; i < 8; i++) out[i] = st[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; i++) out[i] = sha::bswap(st[i]);
+    }
 }
 
 // Root and proofs of one object from its n leaf hashes: layer by layer, an odd layer padded
@@ -109,8 +136,13 @@ hipError_t launch_commit(const CommitArgs &a, hipStream_t s) {
     if (a.nobj == 0 || a.n == 0) return hipSuccess;
     if (a.n > (uint32_t)kCommitMaxLeaves || a.slice_len % 4u || !a.leaf) return hipErrorInvalidValue;
     const uint64_t total = (uint64_t)a.nobj * a.n;
-    hipLaunchKernelGGL(commit::leaf_kernel, dim3((uint32_t)((total + 63) / 64)), dim3(64), 0, s, a);
-    hipError_t e = hipGetLastError();
+    const uint64_t T = ((uint64_t)a.slice_len + 4u + 8u) / 64u + 1u;  // blocks per stream
+    const uint64_t nl = (T + commit::kLeafBlocksPerLaunch - 1) / commit::kLeafBlocksPerLaunch, per = (T + nl - 1) / nl;
+    hipError_t e = hipSuccess;
+    for (uint64_t b0 = 0; b0 < T && e == hipSuccess; b0 += per) {
+        hipLaunchKernelGGL(commit::leaf_kernel, dim3((uint32_t)((total + 63) / 64)), dim3(64), 0, s, a, b0, b0 + per);
+        e = hipGetLastError();
+    }
     if (e != hipSuccess || !a.root) return e;
     hipLaunchKernelGGL(commit::tree_kernel, dim3((a.nobj + 63) / 64), dim3(64), 0, s, a);
     return hipGetLastError();

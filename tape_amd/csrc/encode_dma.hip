@@ -87,6 +87,9 @@ constexpr uint32_t kDrop = 0x80000000u;    // offset past every resource: the ra
 #ifndef TEC_DMA_WPE
 #define TEC_DMA_WPE 4     // waves per SIMD the register budget is cut for (4: <= 128 VGPRs)
 #endif
+#ifndef TEC_DMA_KPRIO
+#define TEC_DMA_KPRIO 0   // wave priority of the whole kernel (s_setprio; 2 measured 6 % slower alone)
+#endif
 #ifndef TEC_DMA_STORE_MASK
 #define TEC_DMA_STORE_MASK 1  // per-job chunk filter (te_recover_batch_device); 0: timing builds only
 #endif
@@ -229,6 +232,10 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint8_t *const lds8 = reinterpret_cast<uint8_t *>(lds);
     const uint32_t lds0 = __builtin_amdgcn_groupstaticsize();  // LDS address of the dynamic array
+    // above the commitment kernel's waves: te_encode_commit_batch_host hashes one group while the
+    // next one encodes, and a leaf wave sharing a SIMD would otherwise halve the encode there
+    // (a copy window's D2H waits for its encode)
+    if constexpr (TEC_DMA_KPRIO) __builtin_amdgcn_s_setprio(TEC_DMA_KPRIO);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
 
@@ -429,7 +436,7 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
                 case 8: col1<8>(acc + 3, sl, stg); break;
                 default: col1<9>(acc + 3, sl, stg); break;
             }
-            if constexpr (TEC_DMA_PRIO) __builtin_amdgcn_s_setprio(0);
+            if constexpr (TEC_DMA_PRIO) __builtin_amdgcn_s_setprio(TEC_DMA_KPRIO);
             if constexpr (!(TEC_DMA_ABLATE & 16)) lds_barrier();  // B2: the plane's rows are staged
             // ---- flush: this wave's share, read now, stored after B1 ----
             const FlushTab::W &F = kFlush.w[type][s][wv];

@@ -319,6 +319,10 @@ struct te_clay {
         DevBuf in, out;
         DevBuf commit;  // te_encode_commit_batch_host: the window's leaf hashes, roots, proofs
     } pipe[kPipe];
+    // encode + commit pipeline streams on disjoint CU sets (commit_streams): hashing on a few
+    // CUs, slot streams (copies, encodes) on the rest
+    hipStream_t cm_ss[2] = {}, cm_hs = nullptr;
+    bool cm_tried = false;
 };
 
 // Drain and free everything a handle holds on its device (on that device).
@@ -351,6 +355,11 @@ static void release_device_state(te_clay *c) {
     c->rec_pending = false;
     if (c->stream) (void)hipStreamDestroy(c->stream);
     c->stream = nullptr;
+    for (hipStream_t *ps : {&c->cm_ss[0], &c->cm_ss[1], &c->cm_hs}) {
+        if (*ps) (void)hipStreamSynchronize(*ps), (void)hipStreamDestroy(*ps);
+        *ps = nullptr;
+    }
+    c->cm_tried = false;
     for (auto &sl : c->pipe) {
         sl.arena.release();
         sl.in.release();
@@ -1848,6 +1857,48 @@ static void group_need(const CommitBatch &B, const CommitPlan &L, size_t x, uint
     rows = L.gcut[x + 1] - L.gcut[x];
 }
 
+// The streams of the encode + commit pipeline (handle locked, its device current): two slot
+// streams and the hashing stream.  A leaf wave that shares a SIMD with an encode wave halves the
+// encode workgroup there, and a copy window's D2H waits for its encode, so the hashing runs on
+// kCommitHashCUs CUs of its own and the slot streams on the others (hipExtStreamCreateWithCUMask).
+// Without CU masking (or if it fails) the handle's pipe streams and its own stream serve.
+static int commit_streams(te_clay *c, hipStream_t ss[2], hipStream_t &hs) {
+    int hash_cus = 32;
+    if (const char *e = tec_knob("TEC_COMMIT_HASH_CUS")) hash_cus = atoi(e);
+    if (hash_cus > 0 && !c->cm_tried) {
+        c->cm_tried = true;
+        hipDeviceProp_t prop{};
+        int ncu = 0;
+        if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) ncu = prop.multiProcessorCount;
+        if (ncu > 2 * hash_cus) {
+            const uint32_t words = (uint32_t)(ncu + 31) / 32;
+            std::vector<uint32_t> hm(words, 0), sm(words, 0);
+            for (int i = 0; i < ncu; i++) (i < hash_cus ? hm : sm)[i / 32] |= 1u << (i % 32);
+            bool ok = hipExtStreamCreateWithCUMask(&c->cm_hs, words, hm.data()) == hipSuccess;
+            for (int k = 0; k < 2 && ok; k++) ok = hipExtStreamCreateWithCUMask(&c->cm_ss[k], words, sm.data()) == hipSuccess;
+            if (!ok)
+                for (hipStream_t *ps : {&c->cm_ss[0], &c->cm_ss[1], &c->cm_hs}) {
+                    if (*ps) (void)hipStreamDestroy(*ps);
+                    *ps = nullptr;
+                }
+            (void)hipGetLastError();
+        }
+    }
+    if (hash_cus > 0 && c->cm_hs) {
+        ss[0] = c->cm_ss[0];
+        ss[1] = c->cm_ss[1];
+        hs = c->cm_hs;
+        return TE_OK;
+    }
+    for (int k = 0; k < 2; k++)
+        if (!c->pipe[k].s) TE_HIP(hipStreamCreateWithFlags(&c->pipe[k].s, hipStreamNonBlocking));
+    if (!c->stream) TE_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    ss[0] = c->pipe[0].s;
+    ss[1] = c->pipe[1].s;
+    hs = c->stream;
+    return TE_OK;
+}
+
 static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_data,
                                    const te_object *objs, size_t nobj, uint8_t *h_out, size_t group_bytes,
                                    const CommitOut &co) {
@@ -1870,16 +1921,12 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
     TE_HIP(dg.err);
-    for (auto &sl : c->pipe)
-        if (!sl.s) TE_HIP(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
-    // the hashing runs on the handle's own stream (idle here: the handle is locked), so the call
-    // uses four streams -- the process's four hardware queues; a fifth stream shared a queue with
-    // a slot stream in bench.py (9.5 against 12.1 GiB/s in a process with no other streams)
-    if (!c->stream) TE_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    // three streams: two slot streams and the hashing stream (a fifth stream beside the caller's
+    // shared a hardware queue with a slot stream in bench.py: 9.5 against 12.1 GiB/s)
     CommitPipe P;
-    P.hs = c->stream;
+    static_assert(CommitPipe::S == 2, "commit_streams makes two slot streams");
+    if ((rc = commit_streams(c, P.ss, P.hs))) return rc;
     for (int k = 0; k < CommitPipe::S; k++) {
-        P.ss[k] = c->pipe[k].s;
         P.in[k] = &c->pipe[k].in;
         P.arena[k] = &c->pipe[k].arena;
     }
@@ -1904,8 +1951,8 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
         if (!rc) rc = group_add(c, cfg, P, G, B, L, x, x + 1 == ngroups);
         if (!rc) rc = group_close(P, G, B.n, B.co.height, B.leaf_b, B.proof_b);
     }
-    for (auto &sl : c->pipe) {
-        const int r2 = hip_status(hipStreamSynchronize(sl.s));
+    for (int k = 0; k < CommitPipe::S; k++) {
+        const int r2 = hip_status(hipStreamSynchronize(P.ss[k]));
         if (rc == TE_OK) rc = r2;
     }
     const int r2 = hip_status(hipStreamSynchronize(P.hs));
@@ -2073,11 +2120,7 @@ int te_stream_writer_new(te_clay *const *coders, size_t ncoders, const te_slicer
             // note); calls on the handle serialise with the writer's windows on them
             te_clay *c = coders[i];
             std::lock_guard<std::mutex> lk(c->mu);
-            for (int k = 0; k < CommitPipe::S && !rc; k++)
-                if (!c->pipe[k].s) rc = hip_status(hipStreamCreateWithFlags(&c->pipe[k].s, hipStreamNonBlocking));
-            if (!rc && !c->stream) rc = hip_status(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-            for (int k = 0; k < CommitPipe::S; k++) d->ss[k] = c->pipe[k].s;
-            d->hs = c->stream;
+            rc = commit_streams(c, d->ss, d->hs);
         }
         CommitPipe &P = d->P;
         P.hs = d->hs;
