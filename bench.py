@@ -553,7 +553,7 @@ def copy_inclusive_commit(args, torch, dist, world, slicer, batch, d_in, d_out, 
     proof = torch.empty(m * N * H * 32, dtype=torch.uint8).pin_memory()
     objs = batch.encode_descs([(i * L, L, i * per, 0) for i in range(m)])
     res = {}
-    for wgib in (2, 4):
+    for wgib in (2, 4, 8):
         wb = wgib << 30
         batch.encode_commit_batch_host(slicer, h_in, objs, h_out, leaf, root, proof, window_bytes=wb)  # warm-up
         if world > 1:
@@ -575,7 +575,10 @@ def copy_inclusive_commit(args, torch, dist, world, slicer, batch, d_in, d_out, 
     # shape (sdk/src/stream/write.rs:332-362): windows of `wobj` objects, at most 4 in flight (the
     # SDK's FuturesOrdered depth), each waited for in order before the 5th is submitted
     stream = {}
-    sw = batch.StreamWriter([slicer], height=H, group_bytes=4 << 30)
+    # hashing groups of 8 GiB (objects + slices): a leaf launch costs one slice's SHA-256 (~29 ms)
+    # whatever the group size, so a group must hold >= ~13 GiB/s x 29 ms of objects (4 GiB groups
+    # closed at half hold ~116 objects and ran 7.3-12 GiB/s; 8 GiB ones 11.3-13.0)
+    sw = batch.StreamWriter([slicer], height=H, group_bytes=8 << 30)
 
     def run_stream(wobj):
         wins = [(a, min(m, a + wobj)) for a in range(0, m, wobj)]
@@ -602,7 +605,7 @@ def copy_inclusive_commit(args, torch, dist, world, slicer, batch, d_in, d_out, 
     ok2 = bool(torch.equal(h_out[:per], d_out[:per].cpu()))
     return {"value": best, "unit": "GiB/s", "objects_per_gpu": m, "steps": args.copy_steps, "pinned": True,
             "tree_height": H, "proofs": True, "by_window": res, "matches_device_resident": ok and ok2,
-            "stream_writer": {"in_flight": 4, "group_bytes": 4 << 30, **stream}}
+            "stream_writer": {"in_flight": 4, "group_bytes": 8 << 30, **stream}}
 
 
 def cpu_baseline(args, np, torch, d_in, d_out, per, L):

@@ -269,17 +269,19 @@ int te_encode_commit_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint
  * (sdk/src/stream/write.rs:332-362 keeps up to min(cores, 4) chunk encodes in flight and hands them
  * on in order through FuturesOrdered) as one GPU pipeline per handle.
  *   te_stream_writer_new: over ncoders device-bound handles (one per GPU); window t goes to handle
- *     (t - 1) mod ncoders.  Hashing groups of at most group_bytes (input + output; 0 = 1 GiB),
- *     three resident per handle.  The writer owns its device buffers and runs on the handles'
- *     own streams; the handles must outlive it and must not be re-bound to another device
- *     meanwhile.
+ *     (t - 1) mod ncoders.  Consecutive windows share a hashing group of at most group_bytes
+ *     (input + output; 0 = 8 GiB), hashed once it holds half of that (one leaf launch costs one
+ *     slice's SHA-256, ~29 ms, whatever the group size), three groups resident per handle.  The
+ *     writer owns its device buffers and runs on the handles' own streams; the handles must
+ *     outlive it and must not be re-bound to another device meanwhile.
  *   te_stream_submit: enqueue one window -- te_encode_commit_batch_host's outputs for its objects
  *     (slices at h_out + out_off, leaf hashes, roots, proofs if h_proofs is not NULL) -- and return
  *     its ticket (1, 2, ... in submission order) without waiting for the device: window t+1's
  *     encode overlaps window t's hashing and copies.  Every host buffer of the window must stay
  *     valid (pinned for full overlap) until te_stream_wait has returned for its ticket.
- *   te_stream_wait: complete every window up to `ticket`, in submission order; returns the first
- *     failure among the windows it completes (TE_OK if none).
+ *   te_stream_wait: complete every window up to `ticket`, in submission order (a window whose
+ *     hashing group is still open has it hashed now); returns the first failure among the
+ *     windows it completes (TE_OK if none).
  *   te_stream_writer_free: waits for every window, then frees the writer. */
 typedef struct te_stream_writer te_stream_writer;
 int te_stream_writer_new(te_clay *const *coders, size_t ncoders, const te_slicer_cfg *cfg, uint32_t height,

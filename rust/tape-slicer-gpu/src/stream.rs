@@ -16,7 +16,7 @@ pub struct StreamWriter<'a> {
 }
 
 impl<'a> StreamWriter<'a> {
-    /// group_bytes: hashing group per handle (0 = 1 GiB); height: SLICE_TREE_HEIGHT.
+    /// group_bytes: hashing group per handle (0 = 8 GiB); height: SLICE_TREE_HEIGHT.
     pub fn new(coders: Vec<&'a mut ClayCoder>, group_bytes: usize) -> Self {
         let raws: Vec<*mut ffi::te_clay> = coders.iter().map(|c| c.raw.as_ptr()).collect();
         let cfg = slicer_cfg(&*coders[0], true, 0);

@@ -2105,7 +2105,7 @@ int te_stream_writer_new(te_clay *const *coders, size_t ncoders, const te_slicer
     if (!w) return TE_ERR_OUT_OF_MEMORY;
     w->cfg = *cfg;
     w->height = height;
-    w->group_bytes = group_bytes ? group_bytes : ((size_t)1 << 30);
+    w->group_bytes = group_bytes ? group_bytes : ((size_t)8 << 30);  // see te_stream_writer_new's header note
     int rc = TE_OK;
     for (size_t i = 0; i < ncoders && !rc; i++) {
         auto d = std::make_unique<te_stream_writer::Dev>();
