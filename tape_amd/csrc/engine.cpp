@@ -2286,16 +2286,21 @@ int te_encode_batch_host_multi(te_clay *const *coders, size_t ncoders, const te_
         while (part < ncoders && acc * ncoders >= total * part) cut[part++] = i + 1;
     }
     std::vector<int> rc(ncoders, TE_OK);
+    std::vector<std::string> why(ncoders);  // each worker's te_last_error_detail (thread-local)
     std::vector<std::thread> th;
     for (size_t p = 0; p < ncoders; p++) {
         if (cut[p + 1] <= cut[p]) continue;
         th.emplace_back([&, p] {
             rc[p] = te_encode_batch_host(coders[p], cfg, h_data, objs + cut[p], cut[p + 1] - cut[p], h_out, window_bytes);
+            if (rc[p]) why[p] = g_last_error;
         });
     }
     for (auto &t : th) t.join();
-    for (int r : rc)
-        if (r) return r;
+    for (size_t p = 0; p < ncoders; p++)
+        if (rc[p]) {  // the first failing handle's status and detail, on the calling thread
+            snprintf(g_last_error, sizeof(g_last_error), "%s", why[p].c_str());
+            return rc[p];
+        }
     return TE_OK;
 }
 
