@@ -33,7 +33,9 @@ __device__ __forceinline__ void dma16(u32x4 rs, uint32_t voff, uint32_t soff, ui
 }
 
 // LMODE: 0 packed (kernel), 1 per-row, 2 two-plane contiguous pieces, 3 two-plane split rows
-// SMODE: 0 per-row each plane, 2 two-plane contiguous pieces, 3 two-plane split rows
+// SMODE: 0 per-row each plane, 2 two-plane contiguous pieces, 3 two-plane split rows,
+//        4 split rows: every wave stores its own 256-byte column segment of every row (dword per
+//          lane, the compute layout's words; no staging)
 template <int LMODE, int SMODE, int NW = 6>
 __global__ void __launch_bounds__(NW * 64) skel(const uint8_t *in, uint8_t *out, uint32_t *sink) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -46,7 +48,7 @@ __global__ void __launch_bounds__(NW * 64) skel(const uint8_t *in, uint8_t *out,
     const u32x4 rs = rsrc(src, src_len);
     const __amdgpu_buffer_rsrc_t wb = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)(19 * SLEN + CS), 0x00020000);
     const u32x4 v = {lane, wv, 7u, 9u};
-    constexpr bool TWO = LMODE >= 2 || SMODE >= 2;
+    constexpr bool TWO = LMODE >= 2 || SMODE == 2 || SMODE == 3;
     constexpr uint32_t STEP = TWO ? 2 : 1;
     constexpr uint32_t SLOT = 16 * 2 * 1440 + 1024;
     for (uint32_t z = 0; z < 100; z += STEP) {
@@ -88,7 +90,13 @@ __global__ void __launch_bounds__(NW * 64) skel(const uint8_t *in, uint8_t *out,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         // ---- stores (20 chunks) ----
-        if (SMODE == 0 || SMODE == 3) {
+        if (SMODE == 4) {  // each wave: its 64 words of each of the 20 rows (a lane's 4 columns)
+            const uint32_t col = (wv * 64 + lane) * 4;
+            for (uint32_t c = 0; c < 20; c++) {
+                const uint32_t base = c * SLEN + z * SC;
+                __builtin_amdgcn_raw_buffer_store_b32(v.x, wb, (int)(col + 4 <= SC ? col : 0x80000000u), (int)base, 2);
+            }
+        } else if (SMODE == 0 || SMODE == 3) {
             for (uint32_t c = wv; c < 20; c += NW) {
                 for (uint32_t p = 0; p < STEP; p++) {
                     const uint32_t base = c * SLEN + (z + p) * SC;
@@ -164,5 +172,8 @@ int main() {
     run<3, 3, 12>("L split2, S split2, 12 waves", din, dout, sink, L2p + 8192);
     run<2, 2, 12>("L piece2, S piece2, 12 waves", din, dout, sink, L2p + 8192);
     run<0, 0>("L packed, S row (kernel shape) again", din, dout, sink, L1p);
+    run<0, 4>("L packed, S split words (no staging)", din, dout, sink, L1p);
+    run<0, 4, 12>("L packed, S split words, 12 waves", din, dout, sink, L2p + 8192);
+    run<0, 0>("L packed, S row (kernel shape) 3rd", din, dout, sink, L1p);
     return 0;
 }

@@ -40,12 +40,17 @@ constexpr uint32_t kOwnBlk = 7 * RB;       // 7 own rows, then 9 partner rows; t
 constexpr uint32_t kPartBlk = 9 * RB;      // overhang a region run with those lanes masked off
 constexpr uint32_t kPartBase = kOwnBlk * 16;
 constexpr uint32_t kSlotBytes = (kOwnBlk + kPartBlk) * 16;
-constexpr uint32_t kStageBase = 2 * kSlotBytes;
+#ifndef TEC_DMA_DIRECT
+#define TEC_DMA_DIRECT 0  // 1 (timing builds): no staging -- each compute lane stores its word of every output row
+#endif                    // itself (one barrier per plane, a three-slot ring): 5.70 against 5.03 ms, row
+                          // pieces split between waves store slowly (skeleton: 5.86 against 4.43 ms)
+constexpr uint32_t kRing = TEC_DMA_DIRECT ? 3 : 2;   // ring slots (planes in flight)
+constexpr uint32_t kStageBase = kRing * kSlotBytes;
 #ifndef TEC_DMA_STAGE_ROWS
 #define TEC_DMA_STAGE_ROWS 24
 #endif
 constexpr uint32_t kStageRows = TEC_DMA_STAGE_ROWS;  // < 24: timing builds only
-constexpr uint32_t kLdsBytes = kStageBase + kStageRows * RW;
+constexpr uint32_t kLdsBytes = kStageBase + (TEC_DMA_DIRECT ? 0u : kStageRows * RW);
 static_assert(kLdsBytes <= 81920 - 1024, "two workgroups per CU, with a margin");
 #ifndef TEC_DMA_LDS_PAD
 #define TEC_DMA_LDS_PAD 0  // timing builds only: extra LDS requested (occupancy probes)
@@ -65,6 +70,8 @@ constexpr int kCap = 5;  // flush rows per wave per step
 #define TEC_DMA_LAG 30
 #endif
 constexpr int kStoreLag = TEC_DMA_LAG;
+// DIRECT: a compute wave issues 11..32 word stores per plane (+ 16-bit tail stores in one wave)
+constexpr int kDirectLag = 48;
 static_assert(kStoreLag <= 3 * 2 * kCap && kStoreLag < 64, "stores older than 3 steps must have landed");
 constexpr uint32_t kDrop = 0x80000000u;    // offset past every resource: the range check drops it
 #ifndef TEC_DMA_PRIO
@@ -89,6 +96,9 @@ constexpr uint32_t kDrop = 0x80000000u;    // offset past every resource: the ra
 #endif
 #ifndef TEC_DMA_KPRIO
 #define TEC_DMA_KPRIO 0   // wave priority of the whole kernel (s_setprio; 2 measured 6 % slower alone)
+#endif
+#ifndef TEC_DMA_LPRIO
+#define TEC_DMA_LPRIO 0   // loader wave priority (s_setprio)
 #endif
 #ifndef TEC_DMA_STORE_MASK
 #define TEC_DMA_STORE_MASK 1  // per-job chunk filter (te_recover_batch_device); 0: timing builds only
@@ -212,16 +222,16 @@ __device__ __forceinline__ void st32(uint8_t *p, uint32_t v) { *reinterpret_cast
 
 // Column 1 of plane (z0, S): u1[j] = U(10+j, (z0, S)).  j < S: the pair with U(10+S, (z0, j))
 // parked at step j finishes (both C's staged); j == S: red, C = U; j > S: park.
-template <int S>
-__device__ __forceinline__ void col1(const uint32_t *u1, uint32_t (&sl)[kSlots], uint8_t *stg) {
+template <int S, class Out>
+__device__ __forceinline__ void col1(const uint32_t *u1, uint32_t (&sl)[kSlots], Out &&out) {
 #pragma unroll
     for (int j = 0; j < S; j++) {
         const uint32_t pu = sl[kSl.slot[j][S]];
         const uint32_t tt = xt(u1[j] ^ pu);
-        st32(stg + (kRowC1 + j) * RW, u1[j] ^ tt);  // C(10+j, (z0, S))
-        st32(stg + (kRowB + j) * RW, pu ^ tt);      // C(10+S, (z0, j))
+        out(kRowC1 + j, u1[j] ^ tt);  // C(10+j, (z0, S))
+        out(kRowB + j, pu ^ tt);      // C(10+S, (z0, j))
     }
-    st32(stg + (kRowC1 + S) * RW, u1[S]);
+    out(kRowC1 + S, u1[S]);
 #pragma unroll
     for (int j = S + 1; j < kQ; j++) sl[kSl.slot[S][j]] = u1[j];
 }
@@ -351,6 +361,26 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
         if (wv == (uint32_t)G) {
             // the loader: every plane's DMA, two planes ahead of the compute; the barriers
             // mirror the compute waves' B2 / B1 (the ring slot of plane z is free after B1 of z)
+            if constexpr (TEC_DMA_LPRIO) __builtin_amdgcn_s_setprio(TEC_DMA_LPRIO);
+            if constexpr (TEC_DMA_DIRECT) {
+                // three slots: plane z + 3 goes into plane z's slot after B1 of z; before B1 of
+                // z, plane z + 1 must have landed (plane z + 2's 23 pieces may still be in flight)
+                issue_dma(0, 0);
+                issue_dma(1, kSlotBytes);
+                issue_dma(2, 2 * kSlotBytes);
+                asm volatile("s_waitcnt vmcnt(46)\n\ts_barrier" ::: "memory");  // plane 0 landed
+                uint32_t sl3 = 0;  // z % 3
+                for (uint32_t z = 0; z < (uint32_t)(kQ * kQ); z++) {
+                    if (z + 2u < (uint32_t)(kQ * kQ))
+                        asm volatile("s_waitcnt vmcnt(23)" ::: "memory");
+                    else
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    lds_barrier();  // B1
+                    if (z + 3u < (uint32_t)(kQ * kQ)) issue_dma(z + 3u, sl3 * kSlotBytes);
+                    sl3 = sl3 == 2u ? 0u : sl3 + 1u;
+                }
+                return;
+            }
             issue_dma(0, 0);
             issue_dma(1, kSlotBytes);
             asm volatile("s_waitcnt vmcnt(23)\n\ts_barrier" ::: "memory");  // plane 0 landed
@@ -371,13 +401,39 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
 
     uint8_t *const stg = lds8 + kStageBase + colw;
     uint32_t prev_n = 0;  // ORDER 2: rows this wave stored last step (2 store instructions each)
+    // DIRECT: a lane stores its word of each output row itself; the word straddling the row end
+    // (sc = 2 mod 4) is two bytes, stored with a 16-bit store by its wave only
+    const uint32_t vo_w = (threadIdx.x < RB * 4u && colw + 4u <= sc) ? colw : kDrop;
+    const uint32_t tw = sc >> 2;  // the straddling word (when sc % 4 == 2)
+    const bool tail_wave = (sc & 2u) && wv == tw / 64u;
+    const uint32_t vo_t = (threadIdx.x == tw) ? colw : kDrop;
+    uint32_t ring = 0;  // DIRECT: z % 3
     for (uint32_t z0 = 0; z0 < (uint32_t)kQ; z0++) {
         const bool lvl2 = z0 >= (uint32_t)K;
         const uint32_t type = lvl2 ? z0 - (K - 1) : 0u;
         for (uint32_t s = 0; s < (uint32_t)kQ; s++) {
             const uint32_t z = z0 * kQ + s;
-            const uint32_t slot = (z & 1u) * kSlotBytes;
+            const uint32_t slot = TEC_DMA_DIRECT ? ring * kSlotBytes : (z & 1u) * kSlotBytes;
             const uint8_t *img = lds8 + slot + colw;
+            // an output row of this step: staging row `r` (the flush table's numbering) or, DIRECT,
+            // the lane's word straight to its chunk at its plane
+            auto out = [&](int r, uint32_t v) {
+                if constexpr (!TEC_DMA_DIRECT) {
+                    st32(stg + r * RW, v);
+                } else {
+                    uint32_t node, plane;
+                    if (r >= kRowB) node = kQ + s, plane = z0 * kQ + (uint32_t)(r - kRowB);        // C(10+s, (z0, j))
+                    else if (r >= kRowC1) node = kQ + (uint32_t)(r - kRowC1), plane = z;         // C(10+j, (z0, s))
+                    else if (r >= kRowX) node = z0, plane = (uint32_t)(K + r - kRowX) * kQ + s;  // C(z0, (7+i, s))
+                    else node = (uint32_t)(K + r - kRowC0), plane = z;                            // node 7+r
+                    if (TEC_DMA_STORE_MASK && !((store_mask >> node) & 1u)) return;  // a chunk the caller does not keep
+                    const uint32_t so = slice_off(node) + plane * sc;
+                    if (!(TEC_DMA_ABLATE & 1)) {
+                        __builtin_amdgcn_raw_buffer_store_b32(v, rb_dst, (int)vo_w, (int)so, TEC_DMA_ST_AUX);
+                        if (tail_wave) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rb_dst, (int)vo_t, (int)so, TEC_DMA_ST_AUX);
+                    }
+                }
+            };
             // ---- compute ----
             if constexpr (TEC_DMA_PRIO) __builtin_amdgcn_s_setprio(TEC_DMA_PRIO);
             uint32_t own[K], part[kQ];
@@ -385,7 +441,18 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
             for (int x = 0; x < K; x++) own[x] = lds32(img + x * RW);
             if (z == ez) {  // end-row substitution, also patched into the image the flush copies
                 own[ex] = fixw;
-                st32(lds8 + slot + ex * RW + colw, fixw);
+                if constexpr (!TEC_DMA_DIRECT) st32(lds8 + slot + ex * RW + colw, fixw);
+            }
+            if constexpr (TEC_DMA_DIRECT) {  // systematic rows: the input words as they are
+                if (!(TEC_DMA_ABLATE & 1)) {
+#pragma unroll
+                    for (int x = 0; x < K; x++) {
+                        if (TEC_DMA_STORE_MASK && !((store_mask >> x) & 1u)) continue;
+                        const uint32_t so = slice_off((uint32_t)x) + z * sc;
+                        __builtin_amdgcn_raw_buffer_store_b32(own[x], rb_dst, (int)vo_w, (int)so, TEC_DMA_ST_AUX);
+                        if (tail_wave) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)own[x], rb_dst, (int)vo_t, (int)so, TEC_DMA_ST_AUX);
+                    }
+                }
             }
             uint32_t acc[20 - K];
             if (!lvl2) {
@@ -400,7 +467,7 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
                 else enc::mds_rows<K, true, (TEC_DMA_ABLATE & 4) != 0>(u, acc);
 #pragma unroll
                 for (int r = 0; r < 3; r++)
-                    st32(stg + (kRowC0 + r) * RW, acc[r] ^ mulc(kPft.t_p[1], part[K + r]));
+                    out(kRowC0 + r, acc[r] ^ mulc(kPft.t_p[1], part[K + r]));
             } else {
 #pragma unroll
                 for (int x = 0; x < 9; x++) part[x] = lds32(img + kPartBase + x * RW);
@@ -417,26 +484,37 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
                     if (r < 2) {
                         const uint32_t us = part[K + r], up = acc[r];
                         const uint32_t tt = xt(us ^ up);
-                        st32(stg + (kRowX + r) * RW, us ^ tt);                      // C(z0, (7+r, s))
-                        st32(stg + (kRowC0 + r) * RW, (uint32_t)r < i0 ? up ^ tt : up);  // C / U(7+r, (z0, s))
+                        // C(z0, (7+r, s)): a row only for r < i0 (staged unconditionally, flushed
+                        // only then)
+                        if (!TEC_DMA_DIRECT || (uint32_t)r < i0) out(kRowX + r, us ^ tt);
+                        out(kRowC0 + r, (uint32_t)r < i0 ? up ^ tt : up);  // C / U(7+r, (z0, s))
                     } else {
-                        st32(stg + (kRowC0 + r) * RW, acc[r]);
+                        out(kRowC0 + r, acc[r]);
                     }
                 }
             }
             switch (s) {
-                case 0: col1<0>(acc + 3, sl, stg); break;
-                case 1: col1<1>(acc + 3, sl, stg); break;
-                case 2: col1<2>(acc + 3, sl, stg); break;
-                case 3: col1<3>(acc + 3, sl, stg); break;
-                case 4: col1<4>(acc + 3, sl, stg); break;
-                case 5: col1<5>(acc + 3, sl, stg); break;
-                case 6: col1<6>(acc + 3, sl, stg); break;
-                case 7: col1<7>(acc + 3, sl, stg); break;
-                case 8: col1<8>(acc + 3, sl, stg); break;
-                default: col1<9>(acc + 3, sl, stg); break;
+                case 0: col1<0>(acc + 3, sl, out); break;
+                case 1: col1<1>(acc + 3, sl, out); break;
+                case 2: col1<2>(acc + 3, sl, out); break;
+                case 3: col1<3>(acc + 3, sl, out); break;
+                case 4: col1<4>(acc + 3, sl, out); break;
+                case 5: col1<5>(acc + 3, sl, out); break;
+                case 6: col1<6>(acc + 3, sl, out); break;
+                case 7: col1<7>(acc + 3, sl, out); break;
+                case 8: col1<8>(acc + 3, sl, out); break;
+                default: col1<9>(acc + 3, sl, out); break;
             }
             if constexpr (TEC_DMA_PRIO) __builtin_amdgcn_s_setprio(TEC_DMA_KPRIO);
+            if constexpr (TEC_DMA_DIRECT) {
+                // B1 only: every wave is done reading this slot; stores older than ~2 steps have
+                // landed (<= kDirectLag in flight), so the slice rows a later DMA reads back
+                // (level-2 partners, >= 8 steps later) are there
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDirectLag) : "memory");
+                lds_barrier();
+                ring = ring == 2u ? 0u : ring + 1u;
+                continue;
+            }
             if constexpr (!(TEC_DMA_ABLATE & 16)) lds_barrier();  // B2: the plane's rows are staged
             // ---- flush: this wave's share, read now, stored after B1 ----
             const FlushTab::W &F = kFlush.w[type][s][wv];
@@ -493,7 +571,7 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
         }
     }
     // the last plane's left-over row (its staging row is untouched since the last compute)
-    if (wv == 0) {
+    if (!TEC_DMA_DIRECT && wv == 0) {
         const uint32_t it = kFlush.extra, src = it & 0xffu;
         const uint8_t *row = lds8 + kStageBase + src * RW;
         const u32x4 e0 = *reinterpret_cast<const u32x4 *>(row + lo0);
