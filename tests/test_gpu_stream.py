@@ -115,3 +115,30 @@ def test_stream_writer_errors():
     with pytest.raises(T.EngineError):
         sw.wait(1)  # never submitted
     sw.close()
+
+
+def test_stream_writer_shared_group_waits(oracle):
+    """Windows share a hashing group (default group size): a wait on the first window hashes the
+    open group that also holds the second; windows with and without proofs share it; later
+    windows open a new group on the same writer."""
+    s = T.Slicer.clay_default()
+    sw = batch.StreamWriter([s])
+    w1 = _window(oracle, s, [4 * MiB, 5000], 4242)
+    w2 = _window(oracle, s, [2 * MiB + 3], 4343)
+    t1 = sw.submit(w1["in"], w1["objs"], w1["out"], w1["leaf"], w1["root"], w1["proof"])
+    t2 = sw.submit(w2["in"], w2["objs"], w2["out"], w2["leaf"], w2["root"])  # no proofs
+    sw.wait(t1)
+    _check(oracle, w1)
+    sw.wait(t2)
+    from oracle import merkle_oracle as O
+    exp = oracle.slicer_encode(oracle.OracleClay(20, 7, 16), w2["datas"][0].tobytes())
+    leaves, r, _ = O.commit_slices(exp, H)
+    assert w2["out"].numpy().tobytes()[:N * len(exp[0])] == b"".join(exp)
+    assert w2["leaf"].numpy().tobytes()[:N * 32] == b"".join(leaves)
+    assert w2["root"].numpy().tobytes()[:32] == r
+    assert not w2["proof"].numpy().any()
+    w3 = _window(oracle, s, [4 * MiB] * 2, 4444)
+    t3 = sw.submit(w3["in"], w3["objs"], w3["out"], w3["leaf"], w3["root"], w3["proof"])
+    assert t3 == 3
+    sw.close()  # waits for the open group
+    _check(oracle, w3)
