@@ -123,8 +123,9 @@ def main():
     ap.add_argument("--mode", choices=["encode", "repair", "decode", "commit", "recover", "outer"], default="encode")
     ap.add_argument("--segments", type=int, default=16,
                     help="--mode outer: snapshot segments per step (OuterCoder(17, 50), 4 MiB chunks)")
-    ap.add_argument("--cpu-sample", type=int, default=512,
-                    help="objects in the CPU-baseline sample (0 = skip); 512 x 4 MiB is ~12 s of CPU work on 16 threads")
+    ap.add_argument("--cpu-sample", type=int, default=1024,
+                    help="objects in the CPU-baseline sample (0 = skip); 1024 x 4 MiB is ~6-20 s of CPU-thread work "
+                         "(16 threads) and checks every GPU output of the default batch")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = min(16, affinity cores): the GPU box grants 16 host cores per GPU (pool rules)")
     ap.add_argument("--copy-objects", type=int, default=-1,
@@ -632,8 +633,9 @@ def cpu_baseline(args, np, torch, d_in, d_out, per, L):
     single = time.perf_counter() - t
     return {"value": round(m * L / wall / 2**30, 4), "unit": "GiB/s", "cores": thr, "kind": "port",
             "sample": f"{m} x 4 MiB objects (first {m} of the batch), {thr} threads, one object per thread; "
-                      "oracle/clay_oracle.c: per-byte GF(2^8) table lookups, the shape of reed-solomon-erasure's "
-                      "pure-Rust mul_slice",
+                      "oracle/clay_oracle.c: the Clay layering restated in C over an AVX2 nibble-shuffle GF(2^8) "
+                      "region multiply -- the method of reed-solomon-erasure's simd-accel C kernel, which the "
+                      "reference's Cargo.lock enables (cc + libc resolved)",
             "single_thread_GiBps": round(L / single / 2**30, 4), "affinity_cores": cores,
             "gpu_matches_oracle_on_sample": match}
 

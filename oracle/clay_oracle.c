@@ -26,6 +26,7 @@
  *      sub-chunks = planes with z_vec[y_lost] == x_lost, ascending.
  *   A7 decode pads the erasure set with the lowest parity nodes >= k+nu up to m.
  */
+#include <immintrin.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -105,12 +106,39 @@ static int rs_build_matrix(int data, int total, uint8_t *out /* stride OC_MAXQT 
     return 0;
 }
 
-/* dst[i] ^= c * src[i] */
+/* dst[i] ^= c * src[i]: reed-solomon-erasure's region multiply.  The reference builds that crate
+ * with its `simd-accel` feature (Cargo.lock:5374-5385 resolves its optional `cc` + `libc`
+ * dependencies), whose C kernel multiplies 32 bytes at a time through two 16-entry nibble tables
+ * and byte shuffles; this is the same method with AVX2 (the Makefile targets x86-64-v3), so the
+ * CPU baseline runs at the reference's speed class rather than a per-byte table walk. */
 static void mul_add(uint8_t *dst, const uint8_t *src, uint8_t c, size_t len) {
     if (!c) return;
-    if (c == 1) { for (size_t i = 0; i < len; i++) dst[i] ^= src[i]; return; }
+    size_t i = 0;
+    if (c == 1) {
+        for (; i + 32 <= len; i += 32) {
+            const __m256i d = _mm256_loadu_si256((const __m256i *)(dst + i));
+            _mm256_storeu_si256((__m256i *)(dst + i), _mm256_xor_si256(d, _mm256_loadu_si256((const __m256i *)(src + i))));
+        }
+        for (; i < len; i++) dst[i] ^= src[i];
+        return;
+    }
     const uint8_t *row = GF_MUL[c];
-    for (size_t i = 0; i < len; i++) dst[i] ^= row[src[i]];
+    uint8_t lo[16], hi[16];
+    for (int v = 0; v < 16; v++) {
+        lo[v] = row[v];
+        hi[v] = row[v << 4];
+    }
+    const __m256i tlo = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)lo));
+    const __m256i thi = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)hi));
+    const __m256i m4 = _mm256_set1_epi8(0x0f);
+    for (; i + 32 <= len; i += 32) {
+        const __m256i sv = _mm256_loadu_si256((const __m256i *)(src + i));
+        const __m256i pl = _mm256_shuffle_epi8(tlo, _mm256_and_si256(sv, m4));
+        const __m256i ph = _mm256_shuffle_epi8(thi, _mm256_and_si256(_mm256_srli_epi64(sv, 4), m4));
+        const __m256i d = _mm256_loadu_si256((const __m256i *)(dst + i));
+        _mm256_storeu_si256((__m256i *)(dst + i), _mm256_xor_si256(d, _mm256_xor_si256(pl, ph)));
+    }
+    for (; i < len; i++) dst[i] ^= row[src[i]];
 }
 
 /* ---------------- Clay code (clay-codes 0.1.1 restated) ---------------- */
