@@ -1858,13 +1858,13 @@ static void group_need(const CommitBatch &B, const CommitPlan &L, size_t x, uint
 }
 
 // The streams of the encode + commit pipeline (handle locked, its device current): two slot
-// streams and the hashing stream.  A leaf wave that shares a SIMD with an encode wave halves the
-// encode workgroup there, and a copy window's D2H waits for its encode, so the hashing runs on
-// 64 CUs of its own and the slot streams on the others (hipExtStreamCreateWithCUMask).
-// Without CU masking (or if it fails) the handle's pipe streams and its own stream serve.
+// streams and the hashing stream -- the handle's pipe streams and its own stream.
+// Measurement option (TEC_DEBUG_KNOBS=1 TEC_COMMIT_HASH_CUS=n): hash on n CUs of their own and
+// copy / encode on the rest (hipExtStreamCreateWithCUMask), so no leaf wave shares a SIMD with an
+// encode wave.  Not the default: it measured within the run-to-run spread (scripts/sw_probe.py,
+// DESIGN §4.4), and CU-masked streams are blocking streams (they synchronise with the null stream).
 static int commit_streams(te_clay *c, hipStream_t ss[2], hipStream_t &hs) {
-    // 64 CUs = 256 SIMDs: one leaf wave per SIMD for groups of up to ~800 objects of 20 slices
-    int hash_cus = 64;
+    int hash_cus = 0;
     if (const char *e = tec_knob("TEC_COMMIT_HASH_CUS")) hash_cus = atoi(e);
     if (hash_cus > 0 && !c->cm_tried) {
         c->cm_tried = true;
