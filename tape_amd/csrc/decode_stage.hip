@@ -20,7 +20,7 @@ namespace tec {
 namespace dstage {
 
 // measurement-only ablations (never in a shipped build): bit 0 no scratch loads, bit 1 no MDS
-// products, bit 2 no flush stores, bit 3 no input loads
+// products, bit 2 no flush stores, bit 3 no input loads, bit 4 no barrier and no flush
 #ifndef TEC_DEC_ABLATE
 #define TEC_DEC_ABLATE 0
 #endif
@@ -33,10 +33,16 @@ namespace dstage {
 #ifndef TEC_DEC_COND_LD
 #define TEC_DEC_COND_LD 0  // 1: issue only the loads a step uses (uniform branches); 0: every slot, range-dropped
 #endif
+#ifndef TEC_DEC_DIRECT
+#define TEC_DEC_DIRECT 1  // 1: decoded words stored straight to the data chunks (no staging rows, no barrier)
+#endif
 #ifndef TEC_DEC_WPE
 #define TEC_DEC_WPE 4  // waves per SIMD the register budget is cut for
 #endif
-constexpr int kMaxG = 6;
+#ifndef TEC_DEC_MAXG
+#define TEC_DEC_MAXG 2  // waves per workgroup at most (direct output: 2 measured best, 6 -> 2: 7.48 -> 5.95 ms)
+#endif
+constexpr int kMaxG = TEC_DEC_MAXG;
 constexpr uint32_t kMaxLdsRows = 64;  // 2 x staging + zero + trash + slots (G = 6: 96 KB)
 
 // PFT of the supported profiles: U = 3 C ^ 2 Cp = C ^ xt(C ^ Cp), and the inverse has the same
@@ -96,7 +102,7 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
     auto rot = [&](uint32_t v) { return __builtin_amdgcn_alignbyte(v, v, vsh); };
     // LDS rows: two staging buffers of max_out rows (a step stages into buffer st & 1, so one
     // barrier per step suffices), a zero row, a trash row, then the lane-private slots
-    const uint32_t mo = H.max_out, zrow = 2u * mo, trow = zrow + 1u, srow0 = zrow + 2u;
+    const uint32_t mo = TEC_DEC_DIRECT ? 0u : H.max_out, zrow = 2u * mo, trow = zrow + 1u, srow0 = zrow + 2u;
     auto lds_at = [&](uint32_t off) -> uint32_t * { return reinterpret_cast<uint32_t *>(lds8 + off + col_local); };
     *lds_at(zrow * RS) = 0u;  // lane-private: read back only by this lane
     // flush: staging row i -> data chunk x at the item's plane, the whole row by one wave
@@ -152,11 +158,38 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
     // a produced value's 10-bit location -> LDS row offset (trash row for none / scratch)
     auto dst_lds = [&](uint32_t f, uint32_t sbase) -> uint32_t {
         const uint32_t ty = (f >> 8) & 3u, ix = f & 0xffu;
-        const uint32_t row = (f & 0x3ffu) == kLoc10None ? trow : ty == kLocStage ? sbase + ix : ty == kLocSlot ? srow0 + ix : trow;
+        const uint32_t row = (f & 0x3ffu) == kLoc10None ? trow
+                             : ty == kLocStage    ? (TEC_DEC_DIRECT ? trow : sbase + ix)
+                             : ty == kLocSlot     ? srow0 + ix
+                                                  : trow;
         return row * RS;
     };
     auto dst_scr = [&](uint32_t f) -> uint32_t {
         return ((f & 0x3ffu) != kLoc10None && ((f >> 8) & 3u) == kLocScratch) ? (f & 0xffu) * RS : kDrop;
+    };
+
+    // direct mode: a staged destination's data chunk and plane (the step's flush item), as the
+    // row's byte offset in the stripe's output, or kDrop
+    auto vec_out = [&](uint32_t f, uint32_t w) -> uint32_t {
+        const uint32_t ix = f & 0xffu;
+        const uint32_t iw = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((kDpOut + (ix >> 1)) << 2), (int)w);
+        const uint32_t it = (iw >> (16u * (ix & 1u))) & 0xffffu;
+        const bool st = (f & 0x3ffu) != kLoc10None && ((f >> 8) & 3u) == kLocStage;
+        return st ? (it & 0xffu) * (uint32_t)a.out_stride + (it >> 8) * sc : kDrop;
+    };
+    // one decoded word (rotated domain) to its row at `off` (uniform): the lane's loaded bytes at
+    // vcol, rotation undone; a row across the stripe's output share is written byte by byte there
+    const uint32_t unsh = (4u - vsh) & 3u;
+    auto put_out = [&](uint32_t off, uint32_t v) {
+        if (off == kDrop) return;
+        const uint32_t wv_ = __builtin_amdgcn_alignbyte(v, v, unsh);
+        if (off + sc <= olen) {
+            __builtin_amdgcn_raw_buffer_store_b32(wv_, rs_out, (int)vcol, (int)off, TEC_DEC_ST_AUX);
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < 4u; k++)  // bytes past out_len fail the range check
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(wv_ >> (8u * k)), rs_out, (int)(vcol + k), (int)off, 0);
+        }
     };
 
     uint32_t own[NK], part[NK], tkp[NE];
@@ -217,9 +250,15 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
         // known data rows: copies (staging is double-buffered, so any time in the step)
         const uint32_t sbase = (st & 1u) * mo;
         {
-            const uint32_t lk = dst_lds(w_cur >> 16, sbase);
+            if (TEC_DEC_DIRECT) {
+                const uint32_t ok = vec_out(w_cur >> 16, w_cur);
 #pragma unroll
-            for (int j = 0; j < NK; j++) *lds_at(W(lk, kDpKd + j)) = cown[j];
+                for (int j = 0; j < NK; j++) put_out(W(ok, kDpKd + j), cown[j]);
+            } else {
+                const uint32_t lk = dst_lds(w_cur >> 16, sbase);
+#pragma unroll
+                for (int j = 0; j < NK; j++) *lds_at(W(lk, kDpKd + j)) = cown[j];
+            }
         }
         // pair partners' U (read before this step's writes: a location may be rewritten from its
         // consumer step on)
@@ -242,6 +281,10 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
         const uint32_t fa = kd_l ? (w_cur >> 16) : ed_l ? (((w_cur >> 28) == kErPark) ? w_cur : kLoc10None) : w_cur;
         const uint32_t la = dst_lds(fa, sbase), sa = dst_scr(fa);
         const uint32_t lb = dst_lds(w_cur >> 10, sbase), lc = dst_lds(w_cur >> 20, sbase);
+        // direct mode: staged destinations as output rows (A: ed0 of eo words; B: ed1; C: epd)
+        const uint32_t oa = TEC_DEC_DIRECT ? vec_out(w_cur, w_cur) : kDrop;
+        const uint32_t ob = TEC_DEC_DIRECT ? vec_out(w_cur >> 10, w_cur) : kDrop;
+        const uint32_t oc = TEC_DEC_DIRECT ? vec_out(w_cur >> 20, w_cur) : kDrop;
         auto put_a = [&](int i, uint32_t v) {
             *lds_at(W(la, i)) = v;
             const uint32_t so = W(sa, i);
@@ -252,20 +295,30 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
             const uint32_t ek = W(w_cur, kDpEd + e) >> 28;
             if (ek == kErRed) {
                 *lds_at(W(la, kDpEo + e)) = acc[e];
+                if (TEC_DEC_DIRECT) put_out(W(oa, kDpEo + e), acc[e]);
             } else if (ek == kErType1) {
                 const uint32_t c = mulc(kPft.t_u[0], acc[e] ^ ctkp[e]) ^ ctkp[e];
                 put_a(kDpEo + e, c);
                 *lds_at(W(lb, kDpEo + e)) = c;
+                if (TEC_DEC_DIRECT) put_out(W(oa, kDpEo + e), c), put_out(W(ob, kDpEo + e), c);
             } else if (ek == kErPark) {
                 put_a(kDpEd + e, acc[e]);
             } else if (ek == kErFinish) {
-                *lds_at(W(la, kDpEo + e)) = pft3(acc[e], pu[e]);
-                *lds_at(W(lc, kDpEo + e)) = pft3(pu[e], acc[e]);
+                const uint32_t c0 = pft3(acc[e], pu[e]), c1 = pft3(pu[e], acc[e]);
+                *lds_at(W(la, kDpEo + e)) = c0;
+                *lds_at(W(lc, kDpEo + e)) = c1;
+                if (TEC_DEC_DIRECT) put_out(W(oa, kDpEo + e), c0), put_out(W(oc, kDpEo + e), c1);
             }
         }
         load_scr(w_nxt);
         if constexpr (TEC_DEC_PRIO) __builtin_amdgcn_s_setprio(0);
-        lds_barrier();  // the step's rows are staged (and the step before last's flushed)
+        // the step's rows are staged (and the step before last's flushed); ablation bit 4: timing only
+        if constexpr (TEC_DEC_DIRECT != 0 || (TEC_DEC_ABLATE & 16) != 0) {  // nothing staged: no barrier, no flush
+            w_cur = w_nxt;
+            w_nxt = w_nn;
+            continue;
+        }
+        lds_barrier();
         const uint32_t no = W(w_cur, kDpHdr) >> 8;
         const uint32_t r_beg = (wv * no) / G, r_end = ((wv + 1) * no) / G;
         for (uint32_t r = r_beg; r < r_end && !(TEC_DEC_ABLATE & 4); r++) {
@@ -291,7 +344,7 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
 
 }  // namespace dstage
 
-uint32_t decode_stage_rows(uint32_t nslots, uint32_t max_out) { return 2 * max_out + 2 + nslots; }
+uint32_t decode_stage_rows(uint32_t nslots, uint32_t max_out) { return (TEC_DEC_DIRECT ? 0u : 2 * max_out) + 2 + nslots; }
 bool decode_stage_fits(uint32_t nslots, uint32_t max_out) { return decode_stage_rows(nslots, max_out) <= dstage::kMaxLdsRows; }
 bool decode_stage_k(int k) { return k >= 7 && k <= 10; }
 
