@@ -88,16 +88,22 @@ def dist_setup(torch, dist, backend: str):
 KERNELS = {
     "encode": ["tec::dma::enc_dma_kernel<false>"],
     "repair": ["tec::rfold::rep_fold_kernel"],  # every folded instance (lost column x known set)
-    "decode": ["tec_dec_fixed"],  # the pattern kernels (dec_rtc.cpp); --decode-jit off: dec_stage_kernel<7, 6>
+    "decode": ["tec_dec_fixed"],  # the pattern kernels (dec_rtc.cpp); random patterns / --decode-jit off: table-driven
     "commit": ["tec::commit::leaf_kernel", "tec::commit::tree_kernel"],
-    "recover": ["tec::dstage::dec_stage_kernel<7, 6>"],  # the fused decode writing only the lost slices
+    "recover": ["tec::dstage::dec_stage_kernel<7, 2>"],  # the fused decode writing only the lost slices
 }
 
 
-def kernel_names(mode: str, decode_jit: str = "async") -> list:
-    if mode == "decode" and decode_jit == "off":
-        return ["tec::dstage::dec_stage_kernel<7, 6>"]
+def kernel_names(mode: str, decode_jit: str = "async", pattern: str = "worst") -> list:
+    # random survivor sets serve ~1 object per pattern: no pattern reaches a compiled kernel
+    if mode == "decode" and (decode_jit == "off" or pattern == "random"):
+        return ["tec::dstage::dec_stage_kernel<7, 2>"]
     return KERNELS.get(mode, [])
+
+
+def traffic_key(mode: str, pattern: str = "worst") -> str:
+    """profiles/traffic.json entry of a bench line (random-pattern decode has its own)."""
+    return "decode:random" if mode == "decode" and pattern == "random" else mode
 
 
 def rank_objects(rank: int, nobj: int) -> tuple[int, int]:
@@ -330,8 +336,8 @@ def main():
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
-            tj = json.load(open(args.traffic_json)).get(args.mode, {})  # per mode (scripts/traffic.py)
-            if tj.get("objects") == nobj and tj.get("kernels") == kernel_names(args.mode, args.decode_jit):
+            tj = json.load(open(args.traffic_json)).get(traffic_key(args.mode, args.pattern), {})  # scripts/traffic.py
+            if tj.get("objects") == nobj and tj.get("kernels") == kernel_names(args.mode, args.decode_jit, args.pattern):
                 traffic = tj.get("hbm_bytes_per_step")
         except Exception:
             traffic = None

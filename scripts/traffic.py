@@ -19,8 +19,14 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import bench  # noqa: E402
 
 
-def per_step(d, mode):
-    names = bench.kernel_names(mode)
+def names_of(m):
+    """kernel names of a traffic.json key: a bench mode, or mode:pattern (decode:random)."""
+    mode, _, pat = m.partition(":")
+    return bench.kernel_names(mode, "async", pat or "worst")
+
+
+def per_step(d, m):
+    names = names_of(m)
     tot = {}
     for cf in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         per = {}
@@ -45,7 +51,7 @@ def main():
     if "mode" in out:  # the round-1 single-mode layout
         out = {}
     for m in modes:
-        c = per_step(os.path.join(root, m), m)
+        c = per_step(os.path.join(root, m.replace(":", "_")), m)
         if not c:
             print(m, "no counters")
             continue
@@ -55,7 +61,7 @@ def main():
         write_b = c.get("WRITE_SIZE", 0.0) * 1024.0
         out[m] = {
             "objects": objects,
-            "kernels": bench.kernel_names(m),
+            "kernels": names_of(m),
             "hbm_bytes_per_step": int(read_b + write_b),
             "read_bytes": int(read_b),
             "write_bytes": int(write_b),

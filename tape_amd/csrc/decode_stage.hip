@@ -36,6 +36,9 @@ namespace dstage {
 #ifndef TEC_DEC_DIRECT
 #define TEC_DEC_DIRECT 1  // 1: decoded words stored straight to the data chunks (no staging rows, no barrier)
 #endif
+#ifndef TEC_DEC_LDS_TAB
+#define TEC_DEC_LDS_TAB 0  // 1: t0..t3 of each product's table from LDS (one broadcast ds_read_b128)
+#endif
 #ifndef TEC_DEC_WPE
 #define TEC_DEC_WPE 4  // waves per SIMD the register budget is cut for
 #endif
@@ -105,6 +108,18 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
     const uint32_t mo = TEC_DEC_DIRECT ? 0u : H.max_out, zrow = 2u * mo, trow = zrow + 1u, srow0 = zrow + 2u;
     auto lds_at = [&](uint32_t off) -> uint32_t * { return reinterpret_cast<uint32_t *>(lds8 + off + col_local); };
     *lds_at(zrow * RS) = 0u;  // lane-private: read back only by this lane
+    // TEC_DEC_LDS_TAB: the pattern's tables (t0..t3) after the rows, [e][j], copied once; a perm
+    // of two VGPR table halves needs no v_mov (one SGPR operand per VALU instruction on gfx9)
+    typedef uint32_t u32x4t __attribute__((ext_vector_type(4)));
+    const uint32_t tab0 = a.lds_rows * RS;
+    if constexpr (TEC_DEC_LDS_TAB != 0) {
+        const uint32_t *Dg = reinterpret_cast<const uint32_t *>(&a.patterns[J.pattern].D[0][0]);
+        for (uint32_t i = threadIdx.x; i < (uint32_t)(NE * NK * 4); i += G * 64u) {
+            const uint32_t e = i / (NK * 4), r = i - e * (NK * 4), j = r >> 2, k = r & 3u;
+            *reinterpret_cast<uint32_t *>(lds8 + tab0 + i * 4u) = Dg[(e * kGpeMaxKnown + j) * (sizeof(PermTab) / 4) + k];
+        }
+        __syncthreads();
+    }
     // flush: staging row i -> data chunk x at the item's plane, the whole row by one wave
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t nb = lseg >> 4, tail = lseg & 15u;
@@ -271,10 +286,35 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
         for (int e = 0; e < NE; e++) {
             acc[e] = 0;
             if ((W(w_cur, kDpEd + e) >> 28) == kErSkip) continue;
+            if (TEC_DEC_ABLATE & 2) {
 #pragma unroll
-            for (int j = 0; j < NK; j++)
-                if (TEC_DEC_ABLATE & 2) acc[e] ^= sel[j].s0 + e; else
-                acc[e] = perm_mul_acc(acc[e], sel[j], D[e][j].t[0], D[e][j].t[1], D[e][j].t[2], D[e][j].t[3]);
+                for (int j = 0; j < NK; j++) acc[e] ^= sel[j].s0 + e;
+                continue;
+            }
+            // known inputs in pairs: 3 perms and 1.5 XOR3 per product, plus a v_mov per 3-bit perm
+            // when both table halves are SGPRs (one SGPR operand per VALU instruction on gfx9)
+            if constexpr (TEC_DEC_LDS_TAB != 0) {
+                auto tb = [&](int j) { return *reinterpret_cast<const u32x4t *>(lds8 + tab0 + (uint32_t)(e * NK + j) * 16u); };
+#pragma unroll
+                for (int j = 0; j + 1 < NK; j += 2) {
+                    const u32x4t x = tb(j), y = tb(j + 1);
+                    acc[e] = perm_mul2_acc(acc[e], sel[j], x[0], x[1], x[2], x[3], D[e][j].t[4], sel[j + 1], y[0], y[1], y[2],
+                                           y[3], D[e][j + 1].t[4]);
+                }
+                if (NK & 1) {
+                    const u32x4t x = tb(NK - 1);
+                    acc[e] = perm_mul_acc(acc[e], sel[NK - 1], x[0], x[1], x[2], x[3], D[e][NK - 1].t[4]);
+                }
+                continue;
+            }
+#pragma unroll
+            for (int j = 0; j + 1 < NK; j += 2)
+                acc[e] = perm_mul2_acc(acc[e], sel[j], D[e][j].t[0], D[e][j].t[1], D[e][j].t[2], D[e][j].t[3], D[e][j].t[4],
+                                       sel[j + 1], D[e][j + 1].t[0], D[e][j + 1].t[1], D[e][j + 1].t[2], D[e][j + 1].t[3],
+                                       D[e][j + 1].t[4]);
+            if (NK & 1)
+                acc[e] = perm_mul_acc(acc[e], sel[NK - 1], D[e][NK - 1].t[0], D[e][NK - 1].t[1], D[e][NK - 1].t[2],
+                                      D[e][NK - 1].t[3], D[e][NK - 1].t[4]);
         }
         // ---- writes: lane A of a word is its general destination (known: kout; erased: the
         // park location; eo: ed0), B and C the staging-only ed1 / epd ----
@@ -361,7 +401,7 @@ size_t decode_stage_scratch_bytes(const DecArgs &a) {
 
 template <int NK, int G>
 static hipError_t launch_dec_g(const DecArgs &a, uint64_t blocks, hipStream_t s) {
-    const size_t lds = (size_t)a.lds_rows * G * 256u;
+    const size_t lds = (size_t)a.lds_rows * G * 256u + (TEC_DEC_LDS_TAB ? (size_t)(2 * kRepQ - NK) * NK * 16u : 0u);
     hipError_t e = ensure_dyn_lds(reinterpret_cast<const void *>(dstage::dec_stage_kernel<NK, G>), lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((dstage::dec_stage_kernel<NK, G>), dim3((uint32_t)blocks), dim3(G * 64), lds, s, a);

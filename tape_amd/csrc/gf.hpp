@@ -143,17 +143,20 @@ constexpr Pft make_pft() {
 
 inline constexpr Pft kPft = make_pft();
 
-// 2-bit-index v_perm tables for multiplication by a runtime constant: T[i] byte j = c*(j << 2i).
+// v_perm tables for multiplication by a runtime constant, over the byte's bit fields [0,3),
+// [3,6), [6,8): v_perm_b32 picks one of 8 bytes of a register pair per byte lane, so a 3-bit
+// field is one perm.  t[0..1] = c*j for j < 8 (low dword j < 4), t[2..3] = c*(j << 3),
+// t[4] = c*(j << 6) for j < 4.
 struct PermTab {
-    uint32_t t[4];
+    uint32_t t[5];
 };
 constexpr PermTab perm_tab(uint8_t c) {
     PermTab r{};
-    for (int i = 0; i < 4; i++) {
-        uint32_t w = 0;
-        for (int j = 0; j < 4; j++) w |= (uint32_t)gf_mul(c, (uint8_t)(j << (2 * i))) << (8 * j);
-        r.t[i] = w;
-    }
+    constexpr int sh[3] = {0, 3, 6}, n[3] = {8, 8, 4};
+    int w = 0;
+    for (int f = 0; f < 3; f++)
+        for (int j0 = 0; j0 < n[f]; j0 += 4, w++)
+            for (int j = 0; j < 4; j++) r.t[w] |= (uint32_t)gf_mul(c, (uint8_t)((j0 + j) << sh[f])) << (8 * j);
     return r;
 }
 

@@ -4,8 +4,8 @@
 //   * xtime "multiples": x, 2x, 4x, ... are built with 6 VALU ops per doubling and a
 //     compile-time coefficient becomes a straight XOR selection (v_xor3_b32 after isel).  Used
 //     where one input feeds many products (the per-plane MDS) or for tiny constants (2, 3).
-//   * 2-bit v_perm_b32 tables: mul(c, x) = XOR_i perm(T_i, T_i, (x >> 2i) & 0x03030303), with the
-//     four table dwords in SGPRs (compile-time constants, or s_load'ed for run-time matrices).
+//   * v_perm_b32 tables over the byte's 3-, 3- and 2-bit fields: mul(c, x) = XOR of three perms,
+//     with the five table dwords in SGPRs (compile-time constants, or s_load'ed for run-time matrices).
 //     Used for single-use products by "heavy" constants and for run-time (decode) matrices.
 // No MFMA: this is byte-wise finite-field arithmetic, not a float contraction.
 #pragma once
@@ -47,36 +47,50 @@ struct Mult {
     }
 };
 
+// Byte fields of four packed bytes, as v_perm selectors: bits [0,3), [3,6) (one 8-entry table
+// pair each) and [6,8) (a 4-entry table).
 struct Sel {
-    uint32_t s0, s1, s2, s3;
+    uint32_t s0, s1, s2;
     __device__ __forceinline__ Sel() {}
     __device__ __forceinline__ explicit Sel(uint32_t x)
-        : s0(x & 0x03030303u), s1((x >> 2) & 0x03030303u), s2((x >> 4) & 0x03030303u),
-          s3((x >> 6) & 0x03030303u) {}
+        : s0(x & 0x07070707u), s1((x >> 3) & 0x07070707u), s2((x >> 6) & 0x03030303u) {}
 };
 
-__device__ __forceinline__ uint32_t perm_mul(const Sel &s, uint32_t t0, uint32_t t1, uint32_t t2,
-                                             uint32_t t3) {
-    const uint32_t a = __builtin_amdgcn_perm(t0, t0, s.s0);
-    const uint32_t b = __builtin_amdgcn_perm(t1, t1, s.s1);
-    const uint32_t c = __builtin_amdgcn_perm(t2, t2, s.s2);
-    const uint32_t d = __builtin_amdgcn_perm(t3, t3, s.s3);
-    return a ^ b ^ c ^ d;
+__device__ __forceinline__ uint32_t gf_xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-// acc ^ c * x in six VALU: four v_perm and two v_bitop3 XOR3 (the backend does not form XOR3
-// from the plain expression, which costs four v_xor_b32)
+__device__ __forceinline__ uint32_t perm_mul(const Sel &s, uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3,
+                                             uint32_t t4) {
+    return gf_xor3(__builtin_amdgcn_perm(t1, t0, s.s0), __builtin_amdgcn_perm(t3, t2, s.s1),
+                   __builtin_amdgcn_perm(t4, t4, s.s2));
+}
+
+// acc ^ c * x in five VALU: three v_perm and two XOR (v_bitop3 for the three-input one: the
+// backend does not form XOR3 from the plain expression)
 __device__ __forceinline__ uint32_t perm_mul_acc(uint32_t acc, const Sel &s, uint32_t t0, uint32_t t1, uint32_t t2,
-                                                 uint32_t t3) {
-    const uint32_t a = __builtin_amdgcn_perm(t0, t0, s.s0);
-    const uint32_t b = __builtin_amdgcn_perm(t1, t1, s.s1);
-    const uint32_t c = __builtin_amdgcn_perm(t2, t2, s.s2);
-    const uint32_t d = __builtin_amdgcn_perm(t3, t3, s.s3);
-    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(acc, a, b, 0x96), c, d, 0x96);
+                                                 uint32_t t3, uint32_t t4) {
+    const uint32_t a = __builtin_amdgcn_perm(t1, t0, s.s0);
+    const uint32_t b = __builtin_amdgcn_perm(t3, t2, s.s1);
+    const uint32_t c = __builtin_amdgcn_perm(t4, t4, s.s2);
+    return gf_xor3(acc, a, b) ^ c;
+}
+
+// acc ^ c * x ^ d * y in nine VALU (six v_perm, three XOR3)
+__device__ __forceinline__ uint32_t perm_mul2_acc(uint32_t acc, const Sel &sx, uint32_t c0, uint32_t c1, uint32_t c2,
+                                                  uint32_t c3, uint32_t c4, const Sel &sy, uint32_t d0, uint32_t d1,
+                                                  uint32_t d2, uint32_t d3, uint32_t d4) {
+    const uint32_t a = __builtin_amdgcn_perm(c1, c0, sx.s0);
+    const uint32_t b = __builtin_amdgcn_perm(c3, c2, sx.s1);
+    const uint32_t c = __builtin_amdgcn_perm(c4, c4, sx.s2);
+    const uint32_t d = __builtin_amdgcn_perm(d1, d0, sy.s0);
+    const uint32_t e = __builtin_amdgcn_perm(d3, d2, sy.s1);
+    const uint32_t f = __builtin_amdgcn_perm(d4, d4, sy.s2);
+    return gf_xor3(gf_xor3(acc, a, b), gf_xor3(c, d, e), f);
 }
 
 __device__ __forceinline__ uint32_t perm_mul(const Sel &s, const PermTab &t) {
-    return perm_mul(s, t.t[0], t.t[1], t.t[2], t.t[3]);
+    return perm_mul(s, t.t[0], t.t[1], t.t[2], t.t[3], t.t[4]);
 }
 
 // c * x for a compile-time-foldable constant used once.

@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(kGpeWords * kGpePlaneThreads) gpe_kernel(GpeAr
                 const Sel s(u);
 #pragma unroll
                 for (int e = 0; e < MAXE; e++)
-                    if ((uint32_t)e < ner) acc[e] = perm_mul_acc(acc[e], s, PT.D[e][j].t[0], PT.D[e][j].t[1], PT.D[e][j].t[2], PT.D[e][j].t[3]);
+                    if ((uint32_t)e < ner) acc[e] = perm_mul_acc(acc[e], s, PT.D[e][j].t[0], PT.D[e][j].t[1], PT.D[e][j].t[2], PT.D[e][j].t[3], PT.D[e][j].t[4]);
             }
 #pragma unroll
             for (int e = 0; e < MAXE; e++)
@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(kGpeWords * kGpePlaneThreads) repair_kernel(Re
                 const Sel s(u);
 #pragma unroll
                 for (int e = 0; e < MAXE; e++)
-                    if ((uint32_t)e < ner) acc[e] = perm_mul_acc(acc[e], s, PT.D[e][j].t[0], PT.D[e][j].t[1], PT.D[e][j].t[2], PT.D[e][j].t[3]);
+                    if ((uint32_t)e < ner) acc[e] = perm_mul_acc(acc[e], s, PT.D[e][j].t[0], PT.D[e][j].t[1], PT.D[e][j].t[2], PT.D[e][j].t[3], PT.D[e][j].t[4]);
             }
 #pragma unroll
             for (int e = 0; e < MAXE; e++) {

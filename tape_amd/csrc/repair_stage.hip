@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(G * 64, 3) rep_stage_kernel(RepArgs a) {
             const Sel s(u);
 #pragma unroll
             for (int e = 0; e < MAXE; e++)
-                if ((uint32_t)e < ner) acc[e] = perm_mul_acc(acc[e], s, D[e][j].t[0], D[e][j].t[1], D[e][j].t[2], D[e][j].t[3]);
+                if ((uint32_t)e < ner) acc[e] = perm_mul_acc(acc[e], s, D[e][j].t[0], D[e][j].t[1], D[e][j].t[2], D[e][j].t[3], D[e][j].t[4]);
         }
         lds_barrier();  // B1: the previous plane's rows have been read out of staging
 #pragma unroll
