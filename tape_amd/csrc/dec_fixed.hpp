@@ -136,18 +136,27 @@ template <int G, int WB = 4> struct Tile {
         olen = (u32)J.out_len;
     }
     TEC_DFI V ld(u32 node, u32 plane) const { return Lane<WB>::ld(rs_in, vcol, nbase[node] + plane * sc); }
+    // direct output (TEC_DFIX_RAW) stores every word back at the column it was loaded from and the
+    // arithmetic is byte-wise, so words stay in load order; staged rows need column order
+#ifdef TEC_DFIX_RAW
+    TEC_DFI V rot(V v) const { return v; }
+#else
     TEC_DFI V rot(V v) const { return Lane<WB>::rot(v, vsh); }
+#endif
     TEC_DFI V lds_ld(u32 row) const { return *reinterpret_cast<const V *>(lds8 + row * RS + col_local); }
     TEC_DFI void lds_st(u32 row, V v) const { *reinterpret_cast<V *>(lds8 + row * RS + col_local) = v; }
     TEC_DFI V scr_ld(u32 row) const { return Lane<WB>::ld(rs_scr, col_local, row * RS); }
     TEC_DFI void scr_st(u32 row, V v) const { Lane<WB>::template st<0>(v, rs_scr, col_local, row * RS); }
-    // one decoded word straight to data chunk x at plane z: every lane stores the bytes it
-    // loaded at (vcol; a tail lane's rotation undone: its columns overlap its neighbour's, same
-    // values); a word across the stripe's output share is written byte by byte (the range check
-    // drops whole dwords)
+    // one decoded word straight to data chunk x at plane z: every lane stores its word where it
+    // loaded it (vcol: a tail lane's columns overlap its neighbour's, same values); a word across
+    // the stripe's output share is written byte by byte (the range check drops whole dwords)
     TEC_DFI void out_st(u32 x, u32 z, V v) const {
         const u32 o = x * out_stride + z * sc + vcol;
+#ifdef TEC_DFIX_RAW
+        const V w = v;
+#else
         const V w = Lane<WB>::unrot(v, vsh);
+#endif
         if (o + (u32)WB > olen && o < olen) {
             for (u32 k = 0; k < (u32)WB; k++) __builtin_amdgcn_raw_buffer_store_b8((u8)Lane<WB>::byte(w, k), rs_out, (int)(o + k), 0, 0);
         } else {

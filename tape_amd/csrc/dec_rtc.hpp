@@ -45,6 +45,7 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
     auto lty = [](uint32_t loc) { return loc >> 24; };
     auto lix = [](uint32_t loc) { return loc & 0xffffffu; };
     auto id2 = [](int a, int c) { return std::to_string(a) + "_" + std::to_string(c); };
+    if (direct) s += "#define TEC_DFIX_RAW 1\n";  // words kept in load order (dec_fixed.hpp Tile::rot)
     s += "#include \"dec_fixed.hpp\"\nusing namespace tec::dfix;\n";
     emit("typedef Lane<%d>::V VT;\n#define VZ (Lane<%d>::zero())\n", wb, wb);
     // flush items per step (data chunk x | plane << 8), scalar-loaded after each step's barrier

@@ -36,9 +36,6 @@ namespace dstage {
 #ifndef TEC_DEC_DIRECT
 #define TEC_DEC_DIRECT 1  // 1: decoded words stored straight to the data chunks (no staging rows, no barrier)
 #endif
-#ifndef TEC_DEC_LDS_TAB
-#define TEC_DEC_LDS_TAB 0  // 1: t0..t3 of each product's table from LDS (one broadcast ds_read_b128)
-#endif
 #ifndef TEC_DEC_WPE
 #define TEC_DEC_WPE 4  // waves per SIMD the register budget is cut for
 #endif
@@ -102,24 +99,15 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
         return __builtin_amdgcn_raw_buffer_load_b32(rs_in, (int)vcol, (int)so, 0);
     };
     auto ldopt = [&](uint32_t so) -> uint32_t { return (TEC_DEC_COND_LD && so == 0x80000000u) ? 0u : ldraw(so); };
-    auto rot = [&](uint32_t v) { return __builtin_amdgcn_alignbyte(v, v, vsh); };
+    // staged rows need each word's bytes in column order (the tail lane's load rotated); direct
+    // output stores every word back where it was loaded, and all the arithmetic is byte-wise, so
+    // the loaded order is kept throughout
+    auto rot = [&](uint32_t v) { return TEC_DEC_DIRECT ? v : __builtin_amdgcn_alignbyte(v, v, vsh); };
     // LDS rows: two staging buffers of max_out rows (a step stages into buffer st & 1, so one
     // barrier per step suffices), a zero row, a trash row, then the lane-private slots
     const uint32_t mo = TEC_DEC_DIRECT ? 0u : H.max_out, zrow = 2u * mo, trow = zrow + 1u, srow0 = zrow + 2u;
     auto lds_at = [&](uint32_t off) -> uint32_t * { return reinterpret_cast<uint32_t *>(lds8 + off + col_local); };
     *lds_at(zrow * RS) = 0u;  // lane-private: read back only by this lane
-    // TEC_DEC_LDS_TAB: the pattern's tables (t0..t3) after the rows, [e][j], copied once; a perm
-    // of two VGPR table halves needs no v_mov (one SGPR operand per VALU instruction on gfx9)
-    typedef uint32_t u32x4t __attribute__((ext_vector_type(4)));
-    const uint32_t tab0 = a.lds_rows * RS;
-    if constexpr (TEC_DEC_LDS_TAB != 0) {
-        const uint32_t *Dg = reinterpret_cast<const uint32_t *>(&a.patterns[J.pattern].D[0][0]);
-        for (uint32_t i = threadIdx.x; i < (uint32_t)(NE * NK * 4); i += G * 64u) {
-            const uint32_t e = i / (NK * 4), r = i - e * (NK * 4), j = r >> 2, k = r & 3u;
-            *reinterpret_cast<uint32_t *>(lds8 + tab0 + i * 4u) = Dg[(e * kGpeMaxKnown + j) * (sizeof(PermTab) / 4) + k];
-        }
-        __syncthreads();
-    }
     // flush: staging row i -> data chunk x at the item's plane, the whole row by one wave
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t nb = lseg >> 4, tail = lseg & 15u;
@@ -192,12 +180,10 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
         const bool st = (f & 0x3ffu) != kLoc10None && ((f >> 8) & 3u) == kLocStage;
         return st ? (it & 0xffu) * (uint32_t)a.out_stride + (it >> 8) * sc : kDrop;
     };
-    // one decoded word (rotated domain) to its row at `off` (uniform): the lane's loaded bytes at
-    // vcol, rotation undone; a row across the stripe's output share is written byte by byte there
-    const uint32_t unsh = (4u - vsh) & 3u;
-    auto put_out = [&](uint32_t off, uint32_t v) {
+    // one decoded word (in the lane's load order) to its row at `off` (uniform), at the lane's
+    // load column vcol; a row across the stripe's output share is written byte by byte there
+    auto put_out = [&](uint32_t off, uint32_t wv_) {
         if (off == kDrop) return;
-        const uint32_t wv_ = __builtin_amdgcn_alignbyte(v, v, unsh);
         if (off + sc <= olen) {
             __builtin_amdgcn_raw_buffer_store_b32(wv_, rs_out, (int)vcol, (int)off, TEC_DEC_ST_AUX);
         } else {
@@ -292,21 +278,8 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
                 continue;
             }
             // known inputs in pairs: 3 perms and 1.5 XOR3 per product, plus a v_mov per 3-bit perm
-            // when both table halves are SGPRs (one SGPR operand per VALU instruction on gfx9)
-            if constexpr (TEC_DEC_LDS_TAB != 0) {
-                auto tb = [&](int j) { return *reinterpret_cast<const u32x4t *>(lds8 + tab0 + (uint32_t)(e * NK + j) * 16u); };
-#pragma unroll
-                for (int j = 0; j + 1 < NK; j += 2) {
-                    const u32x4t x = tb(j), y = tb(j + 1);
-                    acc[e] = perm_mul2_acc(acc[e], sel[j], x[0], x[1], x[2], x[3], D[e][j].t[4], sel[j + 1], y[0], y[1], y[2],
-                                           y[3], D[e][j + 1].t[4]);
-                }
-                if (NK & 1) {
-                    const u32x4t x = tb(NK - 1);
-                    acc[e] = perm_mul_acc(acc[e], sel[NK - 1], x[0], x[1], x[2], x[3], D[e][NK - 1].t[4]);
-                }
-                continue;
-            }
+            // when both table halves are SGPRs (one SGPR operand per VALU instruction on gfx9; the
+            // tables in LDS instead, one broadcast ds_read_b128 per product, measured 30 % slower)
 #pragma unroll
             for (int j = 0; j + 1 < NK; j += 2)
                 acc[e] = perm_mul2_acc(acc[e], sel[j], D[e][j].t[0], D[e][j].t[1], D[e][j].t[2], D[e][j].t[3], D[e][j].t[4],
@@ -401,7 +374,7 @@ size_t decode_stage_scratch_bytes(const DecArgs &a) {
 
 template <int NK, int G>
 static hipError_t launch_dec_g(const DecArgs &a, uint64_t blocks, hipStream_t s) {
-    const size_t lds = (size_t)a.lds_rows * G * 256u + (TEC_DEC_LDS_TAB ? (size_t)(2 * kRepQ - NK) * NK * 16u : 0u);
+    const size_t lds = (size_t)a.lds_rows * G * 256u;
     hipError_t e = ensure_dyn_lds(reinterpret_cast<const void *>(dstage::dec_stage_kernel<NK, G>), lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((dstage::dec_stage_kernel<NK, G>), dim3((uint32_t)blocks), dim3(G * 64), lds, s, a);
