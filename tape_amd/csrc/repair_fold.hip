@@ -33,6 +33,12 @@
 #ifndef TEC_RFOLD_WPE
 #define TEC_RFOLD_WPE 4  // 128 VGPRs (52 B/lane spill): 0.567 ms vs 0.63 at 141 VGPRs (1024 x 4 MiB)
 #endif
+#ifndef TEC_RFOLD_DIRECT
+#define TEC_RFOLD_DIRECT 1  // 1: each finished word stored straight to the lost chunk (no staging, no barrier)
+#endif
+#ifndef TEC_RFOLD_MAXG
+#define TEC_RFOLD_MAXG 2  // waves per workgroup at most (direct: 2 measured best; 0.592 -> 0.572 ms, one down 0.590 -> 0.549)
+#endif
 #ifndef TEC_RFOLD_ST_AUX
 #define TEC_RFOLD_ST_AUX 2  // cache policy of the lost-chunk row stores (nt)
 #endif
@@ -41,7 +47,8 @@ namespace tec {
 namespace rfold {
 
 constexpr int kQ = 10, kK = 7, kA = kQ - kK;  // known / aloof nodes of the other column
-constexpr int kMaxG = 6;
+constexpr int kMaxG = TEC_RFOLD_MAXG;
+constexpr uint32_t kStageRows = TEC_RFOLD_DIRECT ? 0u : 2u * kQ;  // LDS rows before the aloof-U rows
 
 // The other column's known set K as a 10-bit mask of positions; its members ascending (kn) and
 // the aloof rest (al).
@@ -202,6 +209,15 @@ __device__ __forceinline__ void rep_fold_body(const RepArgs &a) {
     // missing, two consecutive steps can have planes of equal parity (a shared buffer would be
     // refilled while other waves still store it)
     auto finish = [&](uint32_t p, uint32_t step, const uint32_t *acc, const uint32_t *ccm) {
+        if constexpr (TEC_RFOLD_DIRECT != 0) {  // each word back where the lane loads (vcol)
+#pragma unroll
+            for (int x = 0; x < kQ; x++) {
+                const uint32_t v = (uint32_t)x == xl ? acc[x] : lost_c(ccm[x], acc[x]);
+                const uint32_t plane = YL == 0 ? (uint32_t)x * kQ + p : p * kQ + (uint32_t)x;
+                __builtin_amdgcn_raw_buffer_store_b32(v, rs_out, (int)vcol, (int)(plane * sc), TEC_RFOLD_ST_AUX);
+            }
+            return;
+        }
         uint8_t *const stg = lds8 + (step & 1u) * kQ * RS;
 #pragma unroll
         for (int x = 0; x < kQ; x++) {
@@ -222,7 +238,7 @@ __device__ __forceinline__ void rep_fold_body(const RepArgs &a) {
     };
     // lane-private LDS rows after the staging buffers: aloof node al[i]'s U at plane kn[j]
     auto ua_at = [&](uint32_t i, uint32_t j) {
-        return reinterpret_cast<uint32_t *>(lds8 + (2u * kQ + i * kK + j) * RS + col_local);
+        return reinterpret_cast<uint32_t *>(lds8 + (kStageRows + i * kK + j) * RS + col_local);
     };
 
     // Loads of plane p, issued one plane ahead and unconditionally (a branch around a load makes
@@ -320,7 +336,7 @@ int repair_fold_column(uint32_t q, uint32_t t, uint32_t k, uint32_t beta, uint32
 
 template <int G>
 static hipError_t launch_fold_g(const RepArgs &a, uint64_t blocks, hipStream_t s) {
-    const size_t lds = (size_t)(2 * rfold::kQ + rfold::kA * rfold::kK) * G * 256u;
+    const size_t lds = (size_t)(rfold::kStageRows + rfold::kA * rfold::kK) * G * 256u;
     hipLaunchKernelGGL((rfold::rep_fold_kernel<G>), dim3((uint32_t)blocks), dim3(G * 64), lds, s, a);
     return hipGetLastError();
 }
