@@ -28,9 +28,16 @@
 namespace tec {
 namespace rstage {
 
+#ifndef TEC_REP_DIRECT
+#define TEC_REP_DIRECT 1  // each finished word stored straight to the lost chunk (no staging, no barrier)
+#endif
+#ifndef TEC_REP_MAXG
+#define TEC_REP_MAXG 2  // waves per workgroup at most (6 with staging)
+#endif
+
 constexpr int kQ = 10;        // q of the supported profiles (beta = 10 repair planes)
-constexpr int kMaxG = 6;
-constexpr int kOutRows = kQ;  // lost (red) + q-1 column-mates per plane
+constexpr int kMaxG = TEC_REP_MAXG;
+constexpr int kOutRows = TEC_REP_DIRECT ? 0 : kQ;  // staging: lost (red) + q-1 column-mates per plane
 constexpr int kMaxAloof = 4;
 constexpr int kLdsRows = kOutRows + kMaxAloof * kQ;
 
@@ -57,7 +64,9 @@ __global__ void __launch_bounds__(G * 64, 3) rep_stage_kernel(RepArgs a) {
     if (w >= wps) w = wps - 1;
     const uint32_t col = w * 4u;
     // A word whose high half lies past the sub-chunk (sc = 2 mod 4, last word) would straddle the
-    // end of the last helper row: it loads the dword 2 bytes earlier and rotates.
+    // end of the last helper row: it loads the dword 2 bytes earlier; staged rows need its bytes
+    // rotated into column order, direct stores put it back where it was loaded (the arithmetic
+    // is byte-wise).
     const bool tailw = col + 4u > sc;
     const uint32_t vcol = tailw ? col - 2u : col, vsh = tailw ? 2u : 0u;
     const uint32_t ner = PT.nerased, nkn = PT.nknown;
@@ -66,9 +75,16 @@ __global__ void __launch_bounds__(G * 64, 3) rep_stage_kernel(RepArgs a) {
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc((void *)J.helper[node], 0, J.helper[node] ? (int)(beta * sc) : 0, 0x00020000);
         const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)vcol, (int)(ri * sc), 0);
-        return __builtin_amdgcn_alignbyte(v, v, vsh);
+        return TEC_REP_DIRECT ? v : __builtin_amdgcn_alignbyte(v, v, vsh);
     };
-    auto stage = [&](uint32_t r, uint32_t v) { *reinterpret_cast<uint32_t *>(lds8 + r * RS + col_local) = v; };
+    typedef const __attribute__((address_space(4))) uint32_t cU32;
+    cU32 *oplane_p = nullptr;  // the plane's staging row -> lost-chunk plane map (direct), scalar-loaded
+    auto stage = [&](uint32_t r, uint32_t v) {
+        if constexpr (TEC_REP_DIRECT != 0)
+            __builtin_amdgcn_raw_buffer_store_b32(v, rs_out, (int)vcol, (int)(oplane_p[r] * sc), TEC_REP_ST_AUX);
+        else
+            *reinterpret_cast<uint32_t *>(lds8 + r * RS + col_local) = v;
+    };
 
     // flush: staging row r -> lost-chunk plane (r == 0: z; else the column-mate's swapped plane)
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -140,7 +156,8 @@ __global__ void __launch_bounds__(G * 64, 3) rep_stage_kernel(RepArgs a) {
             for (int e = 0; e < MAXE; e++)
                 if ((uint32_t)e < ner) acc[e] = perm_mul_acc(acc[e], s, D[e][j].t[0], D[e][j].t[1], D[e][j].t[2], D[e][j].t[3], D[e][j].t[4]);
         }
-        lds_barrier();  // B1: the previous plane's rows have been read out of staging
+        if constexpr (TEC_REP_DIRECT == 0) lds_barrier();  // B1: the previous plane's rows have been read out of staging
+        oplane_p = S.oplane;
 #pragma unroll
         for (int e = 0; e < MAXE; e++) {
             if ((uint32_t)e >= ner) continue;
@@ -157,6 +174,7 @@ __global__ void __launch_bounds__(G * 64, 3) rep_stage_kernel(RepArgs a) {
             }
         }
         if constexpr (TEC_REP_PRIO) __builtin_amdgcn_s_setprio(0);
+        if constexpr (TEC_REP_DIRECT != 0) continue;
         lds_barrier();  // B2: the plane's rows are staged
         for (uint32_t r = r_beg; r < r_end; r++) {
             const uint8_t *row = lds8 + r * RS;
