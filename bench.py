@@ -9,7 +9,9 @@ are partitioned across ranks (per-GPU batches, weak scaling), no data-path colle
 
 Also: --mode repair (config 3), --mode decode (config 4, slices 0..12 erased), --mode commit
 (hash_leaf of the 20 slices + merkle root + proofs of every encoded object) and
---mode recover (decode from 7 slices + re-encode, the node's recover path).
+--mode recover (decode from 7 slices + re-encode, the node's recover path) and
+--mode stream (the SDK's stream-write shape -- 64 MiB chunks, encode_with_proofs per
+chunk, at most 4 in flight -- host -> host through te_stream_writer).
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
@@ -126,7 +128,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--objects", type=int, default=1024, help="objects per GPU per step")
     ap.add_argument("--object-bytes", type=int, default=4 * MiB)
-    ap.add_argument("--mode", choices=["encode", "repair", "decode", "commit", "recover", "outer"], default="encode")
+    ap.add_argument("--mode", choices=["encode", "repair", "decode", "commit", "recover", "outer", "stream"],
+                    default="encode")
+    ap.add_argument("--chunk-bytes", type=int, default=64 * MiB,
+                    help="--mode stream: MAX_TRACK_SIZE, the SDK's stream chunk (sdk/src/stream/manifest.rs:22)")
+    ap.add_argument("--stream-chunks", type=int, default=64, help="--mode stream: chunks per rank per pass")
+    ap.add_argument("--in-flight", type=int, default=4,
+                    help="--mode stream: MAX_ENCODE_WORKERS, chunk encodes in flight (sdk/src/stream/write.rs:54-57)")
     ap.add_argument("--segments", type=int, default=16,
                     help="--mode outer: snapshot segments per step (OuterCoder(17, 50), 4 MiB chunks)")
     ap.add_argument("--cpu-sample", type=int, default=1024,
@@ -163,6 +171,8 @@ def main():
 
     if args.mode == "outer":
         return outer_bench(args, torch, dist, world, rank, dev)
+    if args.mode == "stream":
+        return stream_bench(args, torch, dist, world, rank, dev)
     L, nobj = args.object_bytes, args.objects
     slicer = T.Slicer.clay_default()
     g = slicer.geometry(L)
@@ -473,6 +483,156 @@ def outer_bench(args, torch, dist, world, rank, dev):
             "cpu_baseline": None, "outputs_verified": verified, "decode": decode}), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def stream_bench(args, torch, dist, world, rank, dev):
+    """--mode stream: the SDK's stream-write shape.  write_bytes / write_stream cut the
+    stream into MAX_TRACK_SIZE = 64 MiB chunks (sdk/src/stream/write.rs:219, manifest.rs:22); the
+    encode stage keeps at most MAX_ENCODE_WORKERS = 4 chunk encodes in flight and hands them on in
+    order (FuturesOrdered, write.rs:54-57, 332-362); each chunk is one encode_with_proofs (slices,
+    20 leaf hashes, root, proofs; sdk/src/codec/encoder.rs:220-234).  Here: te_stream_writer, one
+    window per chunk, the 5th submitted after the oldest has been waited for; host buffers in a
+    ring of 2 x in-flight slots (the chunk source refills them).  Copy-inclusive: chunk bytes in host
+    memory, slices + commitments back in host memory.  Legs: the library's choice (auto: these
+    9.7 MB slices hash on the host pool as their D2H lands), device hashing forced, pageable host
+    buffers; the CPU baseline is the oracle's encode + hashlib per chunk."""
+    import collections
+    import hashlib
+    import numpy as np
+    import tape_amd as T
+    from tape_amd import batch, merkle
+    CB, nch, depth, H = args.chunk_bytes, args.stream_chunks, args.in_flight, T.SLICE_TREE_HEIGHT
+    s = T.Slicer.clay_default()
+    g = s.geometry(CB)
+    per = N * g.slice_len
+    R = 2 * depth
+    first, _ = rank_objects(rank, nch)
+    d_src = torch.empty(R * CB, dtype=torch.uint8, device=dev)
+    splitmix_fill(torch, d_src, first, R, CB)
+
+    def ring(pinned):
+        def alloc(n):
+            t = torch.empty(n, dtype=torch.uint8)
+            return t.pin_memory() if pinned else t
+        r = {"in": [alloc(CB) for _ in range(R)], "out": [alloc(per) for _ in range(R)],
+             "leaf": [alloc(N * 32) for _ in range(R)], "root": [alloc(32) for _ in range(R)],
+             "proof": [alloc(N * H * 32) for _ in range(R)]}
+        for k in range(R):
+            r["in"][k].copy_(d_src[k * CB:(k + 1) * CB])
+        return r
+
+    descs = [batch.encode_descs([(0, CB, 0, first + c)]) for c in range(nch)]
+
+    def run(sw, r, chunks):
+        inflight = collections.deque()
+        for c in range(chunks):
+            k = c % R
+            if len(inflight) >= depth:
+                sw.wait(inflight.popleft())
+            inflight.append(sw.submit(r["in"][k], descs[c], r["out"][k], r["leaf"][k], r["root"][k], r["proof"][k]))
+        if inflight:
+            sw.wait(inflight[-1])
+
+    def leg(hashing, pinned):
+        r = ring(pinned)
+        sw = batch.StreamWriter([s], height=H, hashing=hashing)
+        run(sw, r, min(nch, R))  # warm-up: buffers, pool
+        if world > 1:
+            dist.barrier()
+        t = time.perf_counter()
+        run(sw, r, nch)
+        el = max_over_ranks(torch, dist, world, time.perf_counter() - t, dev)
+        sw.close()
+        return nch * world * CB / el / 2**30, el, r
+
+    legs, ring_auto = {}, None
+    for name, hashing, pinned in (("auto_pinned", "auto", True), ("host_hash_pinned", "host", True),
+                                  ("device_hash_pinned", "device", True), ("auto_pageable", "auto", False)):
+        v, el, r = leg(hashing, pinned)
+        legs[name] = {"GiBps": round(v, 3), "ms_per_chunk": round(el / nch * 1e3, 2)}
+        if name == "auto_pinned":
+            ring_auto, el_auto = r, el
+        else:
+            del r
+    # the last R chunks of the auto leg: slices against the device-resident Slicer::encode of the
+    # same bytes, leaf hashes against hashlib, root and proofs against the library's host merkle
+    ok = True
+    d_out = torch.empty(per, dtype=torch.uint8, device=dev)
+    for c in range(max(0, nch - R), nch):
+        k = c % R
+        batch.encode_batch(s, d_src[k * CB:(k + 1) * CB], [(0, CB, 0, first + c)], d_out)
+        torch.cuda.synchronize()
+        ok = ok and torch.equal(ring_auto["out"][k], d_out.cpu())
+        lv = ring_auto["leaf"][k].numpy().tobytes()
+        sl = ring_auto["out"][k].numpy()
+        leaves = []
+        for j in range(N):
+            h = hashlib.sha256(b"LEAF")
+            h.update(memoryview(sl[j * g.slice_len:(j + 1) * g.slice_len]))
+            leaves.append(h.digest())
+        ok = ok and lv == b"".join(leaves)
+        ok = ok and ring_auto["root"][k].numpy().tobytes() == merkle.root_from_leaf_hashes(leaves, H)
+        pv = ring_auto["proof"][k].numpy().tobytes()
+        for j in range(N):
+            ok = ok and pv[j * H * 32:(j + 1) * H * 32] == b"".join(merkle.create_proof_from_leaf_hashes(leaves, j, H))
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline_stream(args, ring_auto, CB, R)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "copy-inclusive stream write GiB/s (64 MiB chunks, encode_with_proofs per chunk, <= 4 in flight), "
+                      "1 MI355X",
+            "value": legs["auto_pinned"]["GiBps"], "unit": "GiB/s", "n_gpus": world, "steps": nch, "warmup": min(nch, R),
+            "ms_per_step": round(el_auto / nch * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (SplitMix64 per chunk), host memory in and out (copy-inclusive)",
+            "config": {"workload": f"stream of {nch} x {CB} B chunks per GPU, one encode_with_proofs window per chunk, "
+                                   f"{depth} in flight (te_stream_writer)", "chunk_bytes": CB,
+                       "slice_len": g.slice_len, "in_flight": depth, "profile": "clay(20,7,16)",
+                       "host_hash_threads": batch.host_hash_threads(),
+                       "host_sha_extensions": bool(T.lib.te_host_sha_extensions()),
+                       "parallelism": f"chunks partitioned over {world} GPU(s)"},
+            "legs": legs, "roofline": None, "cpu_baseline": cpu, "outputs_verified": bool(ok)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_stream(args, r, CB, R):
+    """The reference's stream encode on host cores: per chunk the oracle's Slicer::encode (C
+    restatement, AVX2 region multiply) + hashlib SHA-256 leaves + merkle root and proofs (the
+    oracle's), one chunk per thread: on 16 threads (the GPU's host share) and on MAX_ENCODE_WORKERS
+    = 4 threads, the SDK's own concurrency (write.rs:54-57).  Sample: R chunks per thread count."""
+    from concurrent.futures import ThreadPoolExecutor
+    import hashlib
+    from oracle import oracle as O
+    from oracle import merkle_oracle as MO
+    clay = O.OracleClay(20, 7, 16)
+
+    def one(k):
+        sl = O.slicer_encode_np(clay, r["in"][k].numpy())
+        leaves = []
+        for j in range(N):
+            h = hashlib.sha256(b"LEAF")
+            h.update(memoryview(sl[j]))
+            leaves.append(h.digest())
+        root = MO.root_from_leaf_hashes(leaves, 5)
+        _ = [MO.create_proof_from_leaf_hashes(leaves, i, 5) for i in range(N)]
+        return root
+
+    res = {}
+    cores = len(os.sched_getaffinity(0))
+    for thr in (min(16, cores), 4, 1):
+        jobs = list(range(R)) * (2 if thr == 16 else 1) if thr > 1 else [0]
+        t = time.perf_counter()
+        with ThreadPoolExecutor(thr) as ex:
+            roots = list(ex.map(one, jobs))
+        res[thr] = len(jobs) * CB / (time.perf_counter() - t) / 2**30
+    ok = roots[0] == r["root"][0].numpy().tobytes()
+    return {"value": round(res[min(16, cores)], 3), "unit": "GiB/s", "cores": min(16, cores), "kind": "port",
+            "sample": f"{R * 2} x 64 MiB chunks on {min(16, cores)} threads (one chunk per thread): oracle Slicer::encode "
+                      "+ hashlib SHA-256 leaves + merkle root and proofs",
+            "sdk_4_workers_GiBps": round(res[4], 3), "single_thread_GiBps": round(res[1], 3),
+            "affinity_cores": cores, "root_matches_gpu": bool(ok)}
 
 
 def cpu_baseline_commit(args, d_out, per, slice_len, L):

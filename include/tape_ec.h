@@ -291,6 +291,37 @@ int te_stream_submit(te_stream_writer *w, const uint8_t *h_data, const te_object
 int te_stream_wait(te_stream_writer *w, uint64_t ticket);
 void te_stream_writer_free(te_stream_writer *w);
 
+/* Who computes the leaf hashes of te_encode_commit_batch_host / te_stream_submit.  SHA-256 is
+ * sequential within a slice, so the device hashes one slice per lane (~24 MB/s per lane, one leaf
+ * launch ~ one slice's hash time): it wins for groups of many short slices (batches of 4 MiB
+ * objects).  The SDK's stream shape -- 64 MiB chunks (MAX_TRACK_SIZE, sdk/src/stream/manifest.rs:22),
+ * <= 4 encodes in flight (sdk/src/stream/write.rs:54-57), 9.7 MB slices -- is hashed faster by
+ * host cores, as the SDK does (sdk/src/codec/encoder.rs:220-234): the slices are hashed from the
+ * host output buffer by a worker pool (x86 SHA extensions when present) as soon as their D2H copy
+ * has landed.  TE_HASH_AUTO picks per window (stream writer) or per group (one-shot call) from the
+ * slice count, slice length and pool size; the results are identical either way. */
+#define TE_HASH_AUTO 0
+#define TE_HASH_DEVICE 1
+#define TE_HASH_HOST 2
+int te_set_commit_hashing(int mode);  /* process default (writers copy it when created) */
+int te_stream_writer_set_hashing(te_stream_writer *w, int mode);
+/* Host hashing pool size (0 = default: min(16, CPUs in this process's affinity mask)); waits
+ * until the pool is idle. */
+int te_set_host_hash_threads(int threads);
+int te_host_hash_threads(void);
+int te_host_sha_extensions(void);     /* 1 if the host SHA-256 uses the CPU's SHA extensions */
+
+/* Page-locked host memory for the host <-> device entry points (te_encode_*_host, te_stream_submit,
+ * the per-call te_slicer_* / te_clay_* calls): copies from it run at full PCIe rate and need no
+ * driver staging.  The callers of lib/slicer pass pageable Vec<u8>s (sdk/src/track/write.rs:273-308,
+ * network/node/src/features/spool/repair.rs:312-339); a binding fills buffers from here instead
+ * (rust/tape-slicer-gpu PinnedBuf), or pins an existing allocation in place with te_host_register.
+ * Portable: pinned for every device.  Need a HIP device (TE_ERR_NO_DEVICE otherwise). */
+int te_host_alloc(size_t bytes, void **out);
+void te_host_free(void *p);
+int te_host_register(void *p, size_t bytes);
+int te_host_unregister(void *p);
+
 typedef struct te_decode_object {
     uint64_t slices_off;  /* slice i at d_slices + slices_off + i*slice_len */
     uint64_t slice_len;

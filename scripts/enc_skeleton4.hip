@@ -1,0 +1,204 @@
+// enc_skeleton4.hip -- microbenchmark (not product code), fourth series: the memory shape of a
+// row-of-planes encode ("R10").  One workgroup per stripe walks the 10 rows of planes (z0); per
+// plane the loader wave DMAs the 16 input rows (7 own + 9 partner) into a two-slot ring as the
+// production kernel does, the compute waves read their words and keep every output word of the
+// row in VGPRs (13 parity nodes x 10 planes), and at the row's end the outputs go through LDS
+// (a transposition buffer) and leave as one 14,300-byte piece per (node, row).  Systematic
+// pieces: (S) the loader copies each (node, row) as one 14,300-byte global -> global piece, or
+// (R) row stores from the ring per plane (the production kernel's systematic stores).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++20 -o scripts/enc_skeleton4 scripts/enc_skeleton4.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr uint32_t SC = 1430, CS = 100 * SC, SLEN = 5 * CS + 48, NOBJ = 1024, NST = 5;
+constexpr uint32_t OBJ = 4u << 20;
+constexpr uint32_t RW = 1440, RB = 90;
+constexpr uint32_t PIECE = 10 * SC;           // 14,300
+constexpr uint32_t TP = 14336;                // transposition stride per node
+constexpr uint32_t SLOT = 16 * RW;            // ring slot
+constexpr int G = 6;                          // compute waves
+
+__device__ __forceinline__ u32x4 rsrc(const void *p, uint32_t nrec) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    u32x4 r;
+    r.x = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    r.y = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xffffu);
+    r.z = __builtin_amdgcn_readfirstlane(nrec);
+    r.w = 0x00020000u;
+    return r;
+}
+__device__ __forceinline__ void dma16(u32x4 rs, uint32_t voff, uint32_t soff, uint32_t lds) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds), "s"(soff) : "memory");
+}
+__device__ __forceinline__ void bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// SYS: 0 = loader copies systematic pieces global -> global, 1 = row stores from the ring per plane
+// NB: transposition batches per row (nodes per batch = ceil(13 / NB))
+template <int SYS, int NB>
+__global__ void __launch_bounds__((G + 1) * 64, 1) skel(const uint8_t *in, uint8_t *out, uint32_t *sink) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint8_t *lds8 = reinterpret_cast<uint8_t *>(lds);
+    const uint32_t lds0 = __builtin_amdgcn_groupstaticsize();
+    const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t job = blockIdx.x, obj = job / NST, st = job % NST;
+    const uint8_t *src = in + (size_t)obj * OBJ + (size_t)st * 7 * CS;
+    const uint32_t src_len = st + 1 < NST ? 7 * CS : OBJ - (NST - 1) * 7 * CS;
+    uint8_t *dst = out + (size_t)obj * 20 * SLEN + (size_t)st * CS;
+    const u32x4 rs = rsrc(src, src_len);
+    const __amdgpu_buffer_rsrc_t rb_src = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(src), 0, (int)src_len, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wb = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)(19 * SLEN + CS), 0x00020000);
+    constexpr uint32_t TBASE = 2 * SLOT;
+    constexpr int PER = (13 + NB - 1) / NB;
+    auto row_off = [&](uint32_t r, uint32_t z) -> uint32_t {
+        const uint32_t z0 = z / 10;
+        return r < 7 ? r * CS + z * SC : (z0 < 7 ? z0 : 0) * CS + ((r - 7) * 10 + z % 10) * SC;
+    };
+    auto issue = [&](uint32_t z, uint32_t slot) {
+        for (uint32_t i = 0; i < 23; i++) {
+            const uint32_t b = 64 * i + lane, r = b / RB, k = b - r * RB;
+            if (r < 16) dma16(rs, row_off(r, z) + (k * 16 + 16 <= SC ? k * 16 : SC - 16), 0,
+                              __builtin_amdgcn_readfirstlane(lds0 + slot + 1024 * i));
+        }
+    };
+    if (wv == (uint32_t)G) {
+        // loader: DMA two planes ahead; SYS 0: one (node, row) systematic piece copy per plane
+        // step while the row's first 7 planes run
+        issue(0, 0);
+        issue(1, SLOT);
+        asm volatile("s_waitcnt vmcnt(23)\n\ts_barrier" ::: "memory");
+        for (uint32_t z = 0; z < 100; z++) {
+            const uint32_t s = z % 10, z0 = z / 10;
+            if (SYS == 0 && s < 7) {
+                const uint32_t so = s * CS + z0 * PIECE, dof = s * SLEN + z0 * PIECE;
+                u32x4 v[14];
+#pragma unroll
+                for (int i = 0; i < 14; i++) {
+                    const uint32_t b = 64 * i + lane;
+                    const uint32_t o = b < 894 ? (b * 16 + 16 <= PIECE ? b * 16 : PIECE - 16) : 0x80000000u;
+                    v[i] = __builtin_amdgcn_raw_buffer_load_b128(rb_src, (int)o, (int)so, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < 14; i++) {
+                    const uint32_t b = 64 * i + lane;
+                    const uint32_t o = b < 894 ? (b * 16 + 16 <= PIECE ? b * 16 : PIECE - 16) : 0x80000000u;
+                    __builtin_amdgcn_raw_buffer_store_b128(v[i], wb, (int)o, (int)dof, 2);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bar();  // B1: plane z+1 landed, slot of z free
+            if (z + 2 < 100) issue(z + 2, (z & 1) * SLOT);
+            if (s == 9) for (int b = 0; b < 2 * NB; b++) bar();
+        }
+        return;
+    }
+    asm volatile("s_barrier" ::: "memory");
+    const uint32_t w = wv * 64 + lane;
+    const uint32_t col = w < 358 ? 4 * w : 4 * 357;
+    uint32_t acc = 0;
+    for (uint32_t z0 = 0; z0 < 10; z0++) {
+        uint32_t o[13][10];
+#pragma unroll
+        for (int s = 0; s < 10; s++) {
+            const uint32_t z = z0 * 10 + s;
+            const uint8_t *img = lds8 + (z & 1) * SLOT + col;
+            uint32_t x[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) x[r] = *reinterpret_cast<const uint32_t *>(img + r * RW);
+#pragma unroll
+            for (int n = 0; n < 13; n++) o[n][s] = x[n] ^ x[(n + 3) & 15] ^ (x[(n + 7) & 15] << 1);
+            if (SYS == 1) {
+                // each wave stores ~1.2 of the 7 own rows from the ring image (2 b128 per row)
+                for (uint32_t r = wv; r < 7; r += G) {
+#pragma unroll
+                    for (int k = 0; k < 2; k++) {
+                        const uint32_t bk = 64 * k + lane;
+                        const uint32_t bo = bk < RB ? (bk * 16 + 16 <= SC ? bk * 16 : SC - 16) : 0u;
+                        const u32x4 d = *reinterpret_cast<const u32x4 *>(lds8 + (z & 1) * SLOT + r * RW + bo);
+                        __builtin_amdgcn_raw_buffer_store_b128(d, wb, (int)(bk < RB ? bo : 0x80000000u), (int)(r * SLEN + z * SC), 2);
+                    }
+                }
+            }
+            bar();  // B1
+        }
+        // row end: transpose through LDS in NB batches, store 14,300-byte pieces
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            const int n0 = b * PER, n1 = n0 + PER < 13 ? n0 + PER : 13;
+#pragma unroll
+            for (int n = n0; n < n1; n++)
+#pragma unroll
+                for (int s = 0; s < 10; s++)
+                    *reinterpret_cast<uint32_t *>(lds8 + TBASE + (n - n0) * TP + s * 1432 + col) = o[n][s];
+            bar();
+            for (int n = n0 + (int)wv; n < n1; n += G) {
+                const uint32_t dof = (7 + n) * SLEN + z0 * PIECE;
+#pragma unroll
+                for (int i = 0; i < 14; i++) {
+                    const uint32_t bb = 64 * i + lane;
+                    const uint32_t lo = bb < 894 ? (bb * 16 + 16 <= PIECE ? bb * 16 : PIECE - 16) : 0u;
+                    const u32x4 d = *reinterpret_cast<const u32x4 *>(lds8 + TBASE + (n - n0) * TP + lo);
+                    __builtin_amdgcn_raw_buffer_store_b128(d, wb, (int)(bb < 894 ? lo : 0x80000000u), (int)dof, 2);
+                }
+            }
+            bar();
+        }
+        acc ^= o[0][0];
+    }
+    if (acc == 0x12345678u) sink[0] = 1;
+}
+
+template <typename F>
+float timeit(F f, int reps) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    f();
+    float best = 1e9;
+    for (int k = 0; k < 3; k++) {
+        CK(hipEventRecord(e0, 0));
+        for (int r = 0; r < reps; r++) f();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        CK(hipGetLastError());
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (ms / reps < best) best = ms / reps;
+    }
+    return best;
+}
+
+template <int SYS, int NB>
+void run(const char *name, uint8_t *din, uint8_t *dout, uint32_t *sink) {
+    auto fn = skel<SYS, NB>;
+    constexpr int PER = (13 + NB - 1) / NB;
+    const size_t lds = 2 * SLOT + PER * TP;
+    CK(hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipFuncAttributes at;
+    CK(hipFuncGetAttributes(&at, reinterpret_cast<const void *>(fn)));
+    const float t = timeit([&] { hipLaunchKernelGGL(fn, dim3(NOBJ * NST), dim3((G + 1) * 64), lds, 0, din, dout, sink); }, 10);
+    const double alg = (double)NOBJ * OBJ + (double)NOBJ * 20 * SLEN;
+    printf("%-44s lds %6zu vgpr %3d scratch %4zu %8.3f ms %7.1f GB/s alg frac %.3f\n", name, lds, at.numRegs,
+           at.localSizeBytes, t, alg / t / 1e6, alg / t / 1e6 / 8000.0);
+}
+
+int main() {
+    const size_t in_b = (size_t)NOBJ * OBJ, out_b = (size_t)NOBJ * 20 * SLEN;
+    uint8_t *din, *dout;
+    uint32_t *sink;
+    CK(hipMalloc(&din, in_b + (1 << 20)));
+    CK(hipMalloc(&dout, out_b + (1 << 20)));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMemset(din, 0x5a, in_b));
+    run<0, 2>("R10: sys loader pieces, 2 batches", din, dout, sink);
+    run<1, 2>("R10: sys row stores, 2 batches", din, dout, sink);
+    run<0, 3>("R10: sys loader pieces, 3 batches", din, dout, sink);
+    run<0, 2>("R10: sys loader pieces, 2 batches again", din, dout, sink);
+    return 0;
+}

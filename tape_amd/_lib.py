@@ -151,6 +151,15 @@ def _load() -> C.CDLL:
         "te_stream_submit": (i, [vp, vp, C.POINTER(te_object), sz, vp, vp, vp, vp, C.POINTER(u64)]),
         "te_stream_wait": (i, [vp, u64]),
         "te_stream_writer_free": (None, [vp]),
+        "te_stream_writer_set_hashing": (i, [vp, i]),
+        "te_set_commit_hashing": (i, [i]),
+        "te_set_host_hash_threads": (i, [i]),
+        "te_host_hash_threads": (i, []),
+        "te_host_sha_extensions": (i, []),
+        "te_host_alloc": (i, [sz, C.POINTER(vp)]),
+        "te_host_free": (None, [vp]),
+        "te_host_register": (i, [vp, sz]),
+        "te_host_unregister": (i, [vp]),
         "te_decode_batch_device": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_decode_object), u8p, sz,
                                        vp, vp]),
         "te_repair_batch_device": (i, [vp, vp, C.POINTER(te_repair_object), sz, vp, vp]),

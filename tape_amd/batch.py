@@ -81,7 +81,8 @@ class StreamWriter:
     completes every window up to a ticket in submission order.  The window's host buffers (pinned
     for full overlap) are kept referenced here until its ticket has been waited for."""
 
-    def __init__(self, slicers: list[Slicer], height: int = SLICE_TREE_HEIGHT, group_bytes: int = 0):
+    def __init__(self, slicers: list[Slicer], height: int = SLICE_TREE_HEIGHT, group_bytes: int = 0,
+                 hashing: str = "auto"):
         self._cfg = slicers[0]._cfg()
         self._coders = [s.coder for s in slicers]  # the handles outlive the writer
         hs = (C.c_void_p * len(slicers))(*[s.coder.handle.value for s in slicers])
@@ -90,6 +91,13 @@ class StreamWriter:
                "encode")
         self._h = h
         self._keep = {}
+        self.set_hashing(hashing)
+
+    def set_hashing(self, mode: str) -> None:
+        """Who hashes the leaves (te_stream_writer_set_hashing): "auto" (per window, from its slice
+        count and length), "device" (leaf kernel over groups of windows) or "host" (worker pool
+        over the host slices as their D2H copies land -- the SDK's 64 MiB chunk shape)."""
+        _check(lib.te_stream_writer_set_hashing(self._h, HASHING[mode]), "encode")
 
     def submit(self, data, objs, out, leaf_hashes, roots, proofs=None) -> int:
         arr = objs if _is_desc(objs) else encode_descs(objs)
@@ -117,6 +125,23 @@ class StreamWriter:
         self.close()
 
 
+HASHING = {"auto": 0, "device": 1, "host": 2}  # TE_HASH_AUTO / _DEVICE / _HOST
+
+
+def set_commit_hashing(mode: str) -> None:
+    """Process default for te_encode_commit_batch_host and new stream writers (te_set_commit_hashing)."""
+    _check(lib.te_set_commit_hashing(HASHING[mode]), "encode")
+
+
+def set_host_hash_threads(threads: int) -> None:
+    """Host hashing pool size (te_set_host_hash_threads; 0 = min(16, affinity CPUs))."""
+    _check(lib.te_set_host_hash_threads(threads), "encode")
+
+
+def host_hash_threads() -> int:
+    return lib.te_host_hash_threads()
+
+
 def kernel_timing(enable: bool) -> None:
     """te_kernel_timing: record HIP events around every batch call's kernel launches."""
     _check(lib.te_kernel_timing(1 if enable else 0), "kernel timing")
@@ -127,6 +152,27 @@ def kernel_time_ms() -> tuple[float, int]:
     ms, n = C.c_double(0), C.c_uint32(0)
     _check(lib.te_kernel_time_ms(C.byref(ms), C.byref(n)), "kernel timing")
     return ms.value, n.value
+
+
+def host_empty(nbytes: int):
+    """A numpy uint8 array in page-locked host memory (te_host_alloc), freed with the array: the
+    host buffers of encode_batch_host / StreamWriter.submit copy at full PCIe rate from it."""
+    import weakref
+    import numpy as np
+    p = C.c_void_p()
+    _check(lib.te_host_alloc(nbytes, C.byref(p)), "encode")
+    raw = (C.c_uint8 * max(1, nbytes)).from_address(p.value)
+    weakref.finalize(raw, lib.te_host_free, C.c_void_p(p.value))
+    return np.frombuffer(raw, dtype=np.uint8)[:nbytes]
+
+
+def host_register(arr) -> None:
+    """Pin an existing host array in place (te_host_register); undo with host_unregister."""
+    _check(lib.te_host_register(C.c_void_p(_host_ptr(arr)), arr.nbytes), "encode")
+
+
+def host_unregister(arr) -> None:
+    _check(lib.te_host_unregister(C.c_void_p(_host_ptr(arr))), "encode")
 
 
 def _host_ptr(buf) -> int:

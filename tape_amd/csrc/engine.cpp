@@ -25,7 +25,7 @@
 #include <array>
 #include "clay_host.hpp"
 #include "rs16.hpp"
-#include "sha256.hpp"
+#include "host_hash.hpp"
 
 using namespace tec;
 
@@ -1638,6 +1638,9 @@ static int commit_prepare(const te_clay *c, CommitBatch &B) {
         B.slice_len[i] = g.slice_len;
         B.out_bytes[i] = (uint64_t)B.n * g.slice_len;
         if (g.slice_len % 4) return TE_ERR_INVALID_ARG;  // the leaf kernel reads dwords
+        // encode_enqueue's per-object check, made before a window touches a shared group
+        if (g.chunk_size % (size_t)c->h.alpha || g.slice_len > 0xffffffffull || g.chunk_size > 0xffffffffull)
+            return TE_ERR_TOO_MUCH_DATA;
     }
     B.leaf_b = (uint64_t)B.n * TE_HASH_SIZE;
     B.proof_b = B.co.proof ? B.leaf_b * B.co.height : 0;
@@ -1691,6 +1694,8 @@ struct GroupSeg {
     size_t obj0 = 0;         // first object of the segment in its window (host output index)
     uint64_t row0 = 0, cnt = 0, gout_off = 0;
     std::vector<uint64_t> slice_len, out_bytes;
+    const uint8_t *h_out = nullptr;  // the window's host slices (host-hashed groups read them)
+    std::vector<uint64_t> h_off;     // per object: its slices at h_out + h_off
 };
 struct OpenGroup {
     bool open = false;
@@ -1783,9 +1788,11 @@ static int group_add(te_clay *c, const te_slicer_cfg *cfg, CommitPipe &P, OpenGr
         if (!rc && G.slots_used[k]) rc = hip_status(hipEventRecord(P.ev_slot[k], P.ss[k]));
     }
     if (rc) return rc;
+    seg.h_out = B.h_out;
     for (size_t o = i; o < j; o++) {
         seg.slice_len.push_back(B.slice_len[o]);
         seg.out_bytes.push_back(B.out_bytes[o]);
+        seg.h_off.push_back(B.objs[o].out_off);
         G.bytes += B.objs[o].blob_len + B.out_bytes[o];
     }
     G.out_off = dout;
@@ -1798,6 +1805,80 @@ static int group_add(te_clay *c, const te_slicer_cfg *cfg, CommitPipe &P, OpenGr
 // overlaps the hashing: 11.9 -> 12.4-12.6 GiB/s, one box), one leaf/tree launch per run of equal
 // slice lengths across all its segments, then the D2H of each segment's leaf hashes, roots and
 // proofs into its window's host buffers.
+// root_from_leaf_hashes::<height> and create_proof_from_leaf_hashes::<height> of n leaves
+// (lib/crypto/src/merkle/tree.rs:344-358, 397-455) from one set of layers: odd layers padded with
+// EMPTY_ROOTS[level], proof i = the sibling at each level.
+static int host_tree(const uint8_t *leaf, uint32_t n, uint32_t height, uint8_t *root, uint8_t *proof) {
+    if (height == 0 || height > TE_MAX_MERKLE_TREE_HEIGHT || n == 0) return TE_ERR_INVALID_ARG;
+    std::vector<std::array<uint8_t, 32>> cur(n), next;
+    for (uint32_t i = 0; i < n; i++) memcpy(cur[i].data(), leaf + (size_t)i * 32, 32);
+    std::array<uint8_t, 32> empty;
+    sha::empty_root(0, empty.data());
+    for (uint32_t l = 0; l < height; l++) {
+        if (cur.size() % 2) cur.push_back(empty);
+        if (proof)
+            for (uint32_t i = 0; i < n; i++)
+                memcpy(proof + ((size_t)i * height + l) * 32, cur[(i >> l) ^ 1].data(), 32);
+        next.resize(cur.size() / 2);
+        for (size_t j = 0; j < next.size(); j++) sha::hash_pair(cur[2 * j].data(), cur[2 * j + 1].data(), next[j].data());
+        cur.swap(next);
+        std::array<uint8_t, 32> e2;
+        sha::hash_pair(empty.data(), empty.data(), e2.data());
+        empty = e2;
+    }
+    memcpy(root, cur[0].data(), 32);
+    return TE_OK;
+}
+
+// Host-hashed close (host_hash.hpp):the group's slices are hashed from the host output buffers
+// once their D2H copies have landed -- one pool task per slice, the object's root and proofs by
+// whichever of its slice tasks finishes last.  The group buffer is free as soon as the copies are
+// done.  Returns the job the window tickets wait for.
+static int group_close_host(CommitPipe &P, OpenGroup &G, uint32_t n, uint32_t height, int device,
+                            std::shared_ptr<hh::Job> &job) {
+    constexpr int S = CommitPipe::S;
+    if (!G.open) return TE_OK;
+    G.open = false;
+    for (int k = 0; k < S; k++)
+        if (G.slots_used[k]) TE_HIP(hipStreamWaitEvent(P.hs, P.ev_slot[k], 0));
+    TE_HIP(hipEventRecord(P.ev_hashed[G.r], P.hs));
+    P.hashed_pending[G.r] = true;
+    P.groups++;
+    hipEvent_t landed = nullptr;
+    TE_HIP(hipEventCreateWithFlags(&landed, hipEventDisableTiming | hipEventBlockingSync));
+    if (hipError_t e = hipEventRecord(landed, P.hs); e != hipSuccess) {
+        (void)hipEventDestroy(landed);
+        return hip_status(e);
+    }
+    job = std::make_shared<hh::Job>();
+    std::vector<std::function<void()>> tasks;
+    for (const GroupSeg &sg : G.segs) {
+        for (size_t q = 0; q < sg.cnt; q++) {
+            const uint8_t *slices = sg.h_out + sg.h_off[q];
+            const uint64_t slen = sg.slice_len[q];
+            uint8_t *leaf = sg.co.leaf + (sg.obj0 + q) * (uint64_t)n * TE_HASH_SIZE;
+            uint8_t *root = sg.co.root + (sg.obj0 + q) * TE_HASH_SIZE;
+            uint8_t *proof = sg.co.proof ? sg.co.proof + (sg.obj0 + q) * (uint64_t)n * height * TE_HASH_SIZE : nullptr;
+            auto left = std::make_shared<std::atomic<uint32_t>>(n);
+            for (uint32_t i = 0; i < n; i++)
+                tasks.push_back([=, j = job.get()] {
+                    hh::hash_leaf(slices + (uint64_t)i * slen, slen, leaf + (uint64_t)i * TE_HASH_SIZE);
+                    int rc = TE_OK;
+                    if (left->fetch_sub(1) == 1) rc = host_tree(leaf, n, height, root, proof);
+                    j->done(rc);
+                });
+        }
+    }
+    job->add((int64_t)tasks.size());
+    G.segs.clear();
+    if (tasks.empty()) {
+        (void)hipEventDestroy(landed);
+        return TE_OK;
+    }
+    hh::Pool::get().submit_after(landed, device, std::move(tasks));
+    return TE_OK;
+}
+
 static int group_close(CommitPipe &P, OpenGroup &G, uint32_t n, uint32_t height, uint64_t leaf_b, uint64_t proof_b) {
     constexpr int S = CommitPipe::S;
     if (!G.open) return TE_OK;
@@ -1848,6 +1929,20 @@ static int group_close(CommitPipe &P, OpenGroup &G, uint32_t n, uint32_t height,
     P.groups++;
     G.segs.clear();
     return TE_OK;
+}
+
+// Who hashes a group (te_set_commit_hashing / te_stream_writer_set_hashing, TE_HASH_*).  A leaf
+// launch hashes one slice per lane at ~24 MB/s per lane (715,048 B in ~29.5 ms)
+// whatever the number of slices up to ~64k of them; the host pool hashes ~1.5 GB/s per thread.
+// The device wins for many short slices (a batch of 4 MiB objects), the host for few long ones
+// (the SDK's 64 MiB chunks, ~9.7 MB slices, <= 4 in flight: ~0.4 s per leaf launch).
+std::atomic<int> g_commit_hashing{TE_HASH_AUTO};
+bool host_hash_wins(int mode, uint64_t streams, uint64_t max_slice, uint64_t slice_bytes) {
+    if (mode == TE_HASH_HOST) return true;
+    if (mode == TE_HASH_DEVICE) return false;
+    const double dev_s = (double)max_slice / 24e6 * std::max(1.0, (double)streams / 65536.0);
+    const double host_s = (double)slice_bytes / (1.5e9 * hh::Pool::get().threads());
+    return host_s < dev_s;
 }
 
 // The bytes a group of plan L needs in a group buffer, and its commitment rows.
@@ -1945,12 +2040,21 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
     rc = P.make_events();
     const uint64_t row_b = B.leaf_b + TE_HASH_SIZE + B.proof_b;
     OpenGroup G;
+    std::vector<std::shared_ptr<hh::Job>> jobs;
     for (size_t x = 0; x < ngroups && rc == TE_OK; x++) {
         uint64_t need_out, need_rows;
         group_need(B, L, x, need_out, need_rows);
+        uint64_t max_slice = 0;
+        for (size_t o = L.gcut[x]; o < L.gcut[x + 1]; o++) max_slice = std::max<uint64_t>(max_slice, B.slice_len[o]);
+        const bool host = host_hash_wins(g_commit_hashing.load(), need_rows * B.n, max_slice, need_out);
         rc = group_open(P, G, need_out, need_rows, row_b);
-        if (!rc) rc = group_add(c, cfg, P, G, B, L, x, x + 1 == ngroups);
-        if (!rc) rc = group_close(P, G, B.n, B.co.height, B.leaf_b, B.proof_b);
+        if (!rc) rc = group_add(c, cfg, P, G, B, L, x, x + 1 == ngroups && !host);
+        if (!rc && host) {
+            jobs.emplace_back();
+            rc = group_close_host(P, G, B.n, B.co.height, c->device, jobs.back());
+        } else if (!rc) {
+            rc = group_close(P, G, B.n, B.co.height, B.leaf_b, B.proof_b);
+        }
     }
     for (int k = 0; k < CommitPipe::S; k++) {
         const int r2 = hip_status(hipStreamSynchronize(P.ss[k]));
@@ -1958,6 +2062,10 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
     }
     const int r2 = hip_status(hipStreamSynchronize(P.hs));
     if (rc == TE_OK) rc = r2;
+    for (auto &j : jobs) {  // host-hashed groups: their tasks read the output buffers
+        const int r3 = j ? j->wait() : TE_OK;
+        if (rc == TE_OK) rc = r3;
+    }
     P.destroy_events();
     return rc;
 }
@@ -1982,11 +2090,13 @@ struct te_stream_writer {
         // slice's SHA-256 whatever its size: one launch per window capped small windows at
         // 7.3-7.5 GiB/s); tickets whose last group is still open complete when it closes
         OpenGroup G;
+        bool G_host = false;        // the open group is hashed on the host (host_hash.hpp)
         std::vector<uint64_t> pend;
     };
     struct Ticket {
         int dev = -1;
-        hipEvent_t done = nullptr;
+        hipEvent_t done = nullptr;  // its groups' device work (hashing or the copies host hashing reads)
+        std::vector<std::shared_ptr<hh::Job>> jobs;  // host-hashed groups holding its objects
         int rc = TE_OK;
         bool pending = false;  // its last group is the device's open group
     };
@@ -1995,7 +2105,9 @@ struct te_stream_writer {
     uint32_t height = 0;
     bool proofs = true;
     uint64_t group_bytes = 0;
+    int hashing = TE_HASH_AUTO;
     std::mutex mu;
+    std::mutex wait_mu;  // te_stream_wait calls complete tickets one caller at a time
     uint64_t next = 1;                   // next ticket
     std::map<uint64_t, Ticket> tickets;  // submitted, not yet waited
 };
@@ -2009,13 +2121,18 @@ uint64_t writer_row_bytes(const te_stream_writer &w, const te_stream_writer::Dev
 // Hash the device's open group and complete the tickets waiting on it.  Called with w.mu held.
 int writer_close(te_stream_writer &w, te_stream_writer::Dev &d) {
     int rc = TE_OK;
+    std::shared_ptr<hh::Job> job;
     if (d.G.open) {
         uint64_t leaf_b, proof_b;
         (void)writer_row_bytes(w, d, leaf_b, proof_b);
         std::lock_guard<std::mutex> lk(d.c->mu);
         DeviceGuard dg(d.device);
         rc = hip_status(dg.err);
-        if (!rc) rc = group_close(d.P, d.G, (uint32_t)d.c->h.n, w.height, leaf_b, proof_b);
+        if (!rc && d.G_host)
+            rc = group_close_host(d.P, d.G, (uint32_t)d.c->h.n, w.height, d.device, job);
+        else if (!rc)
+            rc = group_close(d.P, d.G, (uint32_t)d.c->h.n, w.height, leaf_b, proof_b);
+        d.G.open = false;
     }
     for (uint64_t t : d.pend) {
         auto it = w.tickets.find(t);
@@ -2023,11 +2140,12 @@ int writer_close(te_stream_writer &w, te_stream_writer::Dev &d) {
         te_stream_writer::Ticket &T = it->second;
         T.pending = false;
         if (!rc) {
+            // after the group's hashing and copies (a ticket spanning several groups re-records)
             DeviceGuard dg(d.device);
-            rc = hip_status(hipEventCreateWithFlags(&T.done, hipEventDisableTiming));
-            if (!rc) rc = hip_status(hipEventRecord(T.done, d.hs));  // after the group's hashing and copies
-            if (rc && T.done) (void)hipEventDestroy(T.done), T.done = nullptr;
+            if (!T.done) rc = hip_status(hipEventCreateWithFlags(&T.done, hipEventDisableTiming));
+            if (!rc) rc = hip_status(hipEventRecord(T.done, d.hs));
         }
+        if (job) T.jobs.push_back(job);
         if (rc && !T.rc) T.rc = rc;
     }
     d.pend.clear();
@@ -2107,6 +2225,7 @@ int te_stream_writer_new(te_clay *const *coders, size_t ncoders, const te_slicer
     w->cfg = *cfg;
     w->height = height;
     w->group_bytes = group_bytes ? group_bytes : ((size_t)8 << 30);  // see te_stream_writer_new's header note
+    w->hashing = g_commit_hashing.load();
     int rc = TE_OK;
     for (size_t i = 0; i < ncoders && !rc; i++) {
         auto d = std::make_unique<te_stream_writer::Dev>();
@@ -2163,8 +2282,16 @@ int te_stream_submit(te_stream_writer *w, const uint8_t *h_data, const te_object
     B.nobj = nobj;
     B.h_out = h_out;
     B.co = CommitOut{h_leaf_hashes, h_roots, h_proofs, w->height};
+    // every per-object check happens here, before the window touches the device's open group
     int rc = commit_prepare(c, B);
-    if (!rc) {
+    auto pend_t = [&] {
+        if (d.pend.empty() || d.pend.back() != t) d.pend.push_back(t);
+        T.pending = true;
+    };
+    if (!rc && nobj == 0) {  // completes after everything queued before it
+        pend_t();
+        rc = writer_close(*w, d);
+    } else if (!rc) {
         CommitPlan L;
         const uint64_t copy_bytes = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)128 << 20, w->group_bytes / 8));
         commit_plan(B, w->group_bytes, copy_bytes, L);
@@ -2172,6 +2299,16 @@ int te_stream_submit(te_stream_writer *w, const uint8_t *h_data, const te_object
         const uint64_t row_b = writer_row_bytes(*w, d, leaf_b, proof_b);
         B.leaf_b = leaf_b;
         B.proof_b = proof_b;
+        // host or device hashing, per window (host_hash_wins): the SDK's 64 MiB chunks hash on the
+        // host, each window a group of its own closed at once; batches of small objects share
+        // device groups
+        uint64_t max_slice = 0, slice_bytes = 0;
+        for (size_t o = 0; o < nobj; o++) {
+            max_slice = std::max<uint64_t>(max_slice, B.slice_len[o]);
+            slice_bytes += B.out_bytes[o];
+        }
+        const bool host = host_hash_wins(w->hashing, (uint64_t)nobj * B.n, max_slice, slice_bytes);
+        if (d.G.open && d.G_host != host) rc = writer_close(*w, d);
         const uint64_t close_at = std::max<uint64_t>(1, w->group_bytes / 2);
         for (size_t x = 0; x + 1 < L.gcut.size() && !rc; x++) {
             uint64_t need_out, need_rows, gbytes = 0;
@@ -2182,48 +2319,39 @@ int te_stream_submit(te_stream_writer *w, const uint8_t *h_data, const te_object
                            G.bytes + gbytes > w->group_bytes))
                 rc = writer_close(*w, d);  // earlier windows' tickets complete with it
             if (rc) break;
+            pend_t();
             {
                 std::lock_guard<std::mutex> lk(c->mu);
                 DeviceGuard dg(d.device);
                 rc = c->device != d.device ? TE_ERR_INVALID_ARG : hip_status(dg.err);  // handle re-bound under the writer
                 if (!rc && !G.open) {
                     // a group buffer holds a full group's slices (group_bytes of objects + slices,
-                    // ~3/4 of it slices for Clay(20, 7)) and its commitment rows
-                    const uint64_t want_out = std::max<uint64_t>(need_out, w->group_bytes - w->group_bytes / 4);
-                    const uint64_t want_rows = std::max<uint64_t>(need_rows, 4096);
+                    // ~3/4 of it slices for Clay(20, 7)) and its commitment rows; a host-hashed
+                    // group holds one window
+                    const uint64_t want_out = host ? need_out : std::max<uint64_t>(need_out, w->group_bytes - w->group_bytes / 4);
+                    const uint64_t want_rows = host ? need_rows : std::max<uint64_t>(need_rows, 4096);
                     rc = group_open(d.P, G, want_out, want_rows, row_b);
+                    d.G_host = host;
                 }
+                // on failure the group keeps its earlier segments (group_add adds one only on
+                // success): the earlier windows still complete below
                 if (!rc) rc = group_add(c, &w->cfg, d.P, G, B, L, x, false);
             }
-            if (!rc && G.bytes >= close_at) rc = writer_close(*w, d);  // pending windows complete with it
+            if (!rc && (host || G.bytes >= close_at)) rc = writer_close(*w, d);  // pending windows complete with it
         }
-        if (!rc) {
-            if (d.G.open) {
-                T.pending = true;
-                d.pend.push_back(t);
-            } else {
-                // this window's last group is hashed (queued): it and any earlier pending windows
-                // complete after it
-                d.pend.push_back(t);
-                T.pending = true;
-                rc = writer_close(*w, d);
-            }
-        }
-        if (rc) {  // groups already enqueued may still read or write the window's host buffers
-            (void)writer_drain(d);
-            d.G.open = false;
-            for (uint64_t pt : d.pend) {
-                auto it = w->tickets.find(pt);
-                if (it != w->tickets.end()) {
-                    it->second.pending = false;
-                    if (!it->second.rc) it->second.rc = rc;
-                }
-            }
-            d.pend.clear();
-            if (T.done) (void)hipEventDestroy(T.done);
-            T.done = nullptr;
-            T.pending = false;
-        }
+    }
+    if (rc) {
+        // only this window fails: the earlier windows of the open group are hashed and complete
+        // normally; then the device is drained, since work already enqueued for this window may
+        // still read or write its host buffers
+        d.pend.erase(std::remove(d.pend.begin(), d.pend.end(), t), d.pend.end());
+        T.pending = false;
+        (void)writer_close(*w, d);
+        (void)writer_drain(d);
+        for (auto &j : T.jobs) (void)j->wait();
+        T.jobs.clear();
+        if (T.done) (void)hipEventDestroy(T.done);
+        T.done = nullptr;
     }
     T.rc = rc;
     return rc;
@@ -2231,21 +2359,22 @@ int te_stream_submit(te_stream_writer *w, const uint8_t *h_data, const te_object
 
 int te_stream_wait(te_stream_writer *w, uint64_t ticket) {
     if (!w || ticket == 0) return TE_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> wg(w->wait_mu);
     int first = TE_OK;
     for (;;) {
-        uint64_t t;
         te_stream_writer::Ticket T;
         {
             std::lock_guard<std::mutex> g(w->mu);
             if (ticket >= w->next) return TE_ERR_INVALID_ARG;  // never submitted
             if (w->tickets.empty() || w->tickets.begin()->first > ticket) return first;
-            t = w->tickets.begin()->first;
             if (w->tickets.begin()->second.pending) {  // its group is still open: hash it now
                 te_stream_writer::Dev &d = *w->devs[(size_t)w->tickets.begin()->second.dev];
                 const int r = writer_close(*w, d);
                 if (r) (void)writer_drain(d);
             }
-            T = w->tickets.begin()->second;
+            // claimed: only this caller (wait_mu) completes it
+            T = std::move(w->tickets.begin()->second);
+            w->tickets.erase(w->tickets.begin());
         }
         int rc = T.rc;
         if (T.done) {
@@ -2254,12 +2383,64 @@ int te_stream_wait(te_stream_writer *w, uint64_t ticket) {
             if (!rc) rc = r;
             (void)hipEventDestroy(T.done);
         }
-        {
-            std::lock_guard<std::mutex> g(w->mu);
-            w->tickets.erase(t);
+        for (auto &j : T.jobs) {
+            const int r = j->wait();
+            if (!rc) rc = r;
         }
         if (!first) first = rc;
     }
+}
+
+int te_stream_writer_set_hashing(te_stream_writer *w, int mode) {
+    if (!w || mode < TE_HASH_AUTO || mode > TE_HASH_HOST) return TE_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(w->mu);
+    w->hashing = mode;
+    return TE_OK;
+}
+
+int te_set_commit_hashing(int mode) {
+    if (mode < TE_HASH_AUTO || mode > TE_HASH_HOST) return TE_ERR_INVALID_ARG;
+    g_commit_hashing.store(mode);
+    return TE_OK;
+}
+
+int te_set_host_hash_threads(int threads) {
+    if (threads < 0) return TE_ERR_INVALID_ARG;
+    return hh::Pool::get().set_threads(threads);
+}
+
+int te_host_hash_threads(void) { return hh::Pool::get().threads(); }
+
+int te_host_sha_extensions(void) { return hh::have_sha_ext() ? 1 : 0; }
+
+int te_host_alloc(size_t bytes, void **out) {
+    if (!out) return TE_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    if (bytes == 0) bytes = 1;
+    void *p = nullptr;
+    const hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocPortable);
+    if (e != hipSuccess) return e == hipErrorOutOfMemory ? TE_ERR_OUT_OF_MEMORY : hip_status(e);
+    *out = p;
+    return TE_OK;
+}
+
+void te_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
+int te_host_register(void *p, size_t bytes) {
+    if (!p || bytes == 0) return TE_ERR_INVALID_ARG;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    TE_HIP(hipHostRegister(p, bytes, hipHostRegisterPortable));
+    return TE_OK;
+}
+
+int te_host_unregister(void *p) {
+    if (!p) return TE_ERR_INVALID_ARG;
+    if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    TE_HIP(hipHostUnregister(p));
+    return TE_OK;
 }
 
 void te_stream_writer_free(te_stream_writer *w) {
@@ -2884,7 +3065,7 @@ int te_clay_repair(te_clay *c, uint32_t lost, const uint32_t *helpers, const uin
 // ---- slice commitments (lib/crypto/src/merkle/tree.rs) ----
 int te_hash_leaf(const uint8_t *data, size_t len, uint8_t out[TE_HASH_SIZE]) {
     if ((!data && len) || !out) return TE_ERR_INVALID_ARG;
-    sha::hash_leaf(data, len, out);
+    hh::hash_leaf(data, len, out);
     return TE_OK;
 }
 

@@ -55,12 +55,14 @@ def _check(oracle, w):
         assert gp == proofs, i
 
 
+@pytest.mark.parametrize("hashing", ["device", "host"])
 @pytest.mark.parametrize("handles,group", [(1, 0), (1, 20 * MiB), (2, 0)])
-def test_stream_writer_windows_in_order(oracle, handles, group):
+def test_stream_writer_windows_in_order(oracle, handles, group, hashing):
     """Four windows submitted before the first wait (one or two handles on device 0; small groups
-    split a window into several hashing groups); waiting on ticket 3 completes 1..3 in order."""
+    split a window into several hashing groups); waiting on ticket 3 completes 1..3 in order.
+    Leaves hashed by the device's leaf kernel or by the host pool (host_hash.hpp)."""
     slicers = [T.Slicer.clay_default() for _ in range(handles)]
-    sw = batch.StreamWriter(slicers, group_bytes=group)
+    sw = batch.StreamWriter(slicers, group_bytes=group, hashing=hashing)
     wins = [_window(oracle, slicers[0], sizes, 1000 * k) for k, sizes in enumerate(
         [[4 * MiB] * 3, [1_000_003, 0, 4 * MiB, 77], [3 * MiB + 5] * 4, [2 * MiB, 4 * MiB + 9]])]
     tickets = [sw.submit(w["in"], w["objs"], w["out"], w["leaf"], w["root"], w["proof"]) for w in wins]
@@ -142,3 +144,90 @@ def test_stream_writer_shared_group_waits(oracle):
     assert t3 == 3
     sw.close()  # waits for the open group
     _check(oracle, w3)
+
+
+@pytest.mark.parametrize("hashing", ["auto", "device"])
+def test_stream_writer_sdk_chunk_shape(oracle, hashing):
+    """The SDK's stream shape (sdk/src/stream/write.rs:54-57, 219, 332-362; manifest.rs:22): a
+    stream cut into MAX_TRACK_SIZE = 64 MiB chunks (the last one short), one encode_with_proofs
+    window per chunk, at most MAX_ENCODE_WORKERS = 4 in flight -- the 5th chunk is submitted only
+    after the oldest has been waited for.  "auto" hashes these 9.7 MB slices on the host pool; the
+    device leaf kernel must give the same bytes."""
+    import collections
+    s = T.Slicer.clay_default()
+    sw = batch.StreamWriter([s], hashing=hashing)
+    sizes = [64 * MiB] * 5 + [13 * MiB + 5] if hashing == "auto" else [64 * MiB, 64 * MiB + 0, 5 * MiB + 3]
+    wins, inflight = [], collections.deque()
+    for k, L in enumerate(sizes):
+        if len(inflight) >= 4:
+            sw.wait(inflight.popleft())
+        w = _window(oracle, s, [L], 90_000 + 17 * k)
+        wins.append(w)
+        inflight.append(sw.submit(w["in"], w["objs"], w["out"], w["leaf"], w["root"], w["proof"]))
+    sw.wait(inflight[-1])
+    for w in wins:
+        _check(oracle, w)
+    sw.close()
+
+
+def test_stream_writer_failed_window_is_isolated(oracle):
+    """A window that fails its checks (an object too large for 32-bit slices: TooMuchData) fails
+    alone: the windows before it, sharing its device's open hashing group, and after it complete
+    with the right bytes (one bad window used to fail every window of the group)."""
+    s = T.Slicer.clay_default()
+    sw = batch.StreamWriter([s], hashing="device")
+    w1 = _window(oracle, s, [4 * MiB, 3 * MiB], 31)
+    w3 = _window(oracle, s, [2 * MiB + 1], 33)
+    t1 = sw.submit(w1["in"], w1["objs"], w1["out"], w1["leaf"], w1["root"], w1["proof"])
+    bad = _window(oracle, s, [16], 32)
+    with pytest.raises(T.EncodeError):
+        sw.submit(bad["in"], [(0, 1 << 40, 0, 0)], bad["out"], bad["leaf"], bad["root"])
+    t3 = sw.submit(w3["in"], w3["objs"], w3["out"], w3["leaf"], w3["root"], w3["proof"])
+    assert (t1, t3) == (1, 3)
+    sw.wait(t1)
+    _check(oracle, w1)
+    with pytest.raises(T.EncodeError):
+        sw.wait(t3)  # completes ticket 2 (failed) and 3
+    _check(oracle, w3)
+    sw.close()
+
+
+def test_host_hashing_one_shot(oracle):
+    """te_encode_commit_batch_host with the host pool forced (te_set_commit_hashing): same slices,
+    leaves, roots and proofs as the oracle; back to auto afterwards."""
+    s = T.Slicer.clay_default()
+    w = _window(oracle, s, [4 * MiB, 1_000_001, 4 * MiB + 8], 4711)
+    batch.set_commit_hashing("host")
+    try:
+        batch.encode_commit_batch_host(s, w["in"], w["objs"], w["out"], w["leaf"], w["root"], w["proof"])
+    finally:
+        batch.set_commit_hashing("auto")
+    _check(oracle, w)
+
+
+def test_pinned_host_buffers(oracle):
+    """te_host_alloc / te_host_register: encode_batch_host from and into pinned
+    buffers the library allocated, and from a pageable array pinned in place, equal the oracle."""
+    s = T.Slicer.clay_default()
+    sizes = [4 * MiB, 1_234_567]
+    geo = [s.geometry(L) for L in sizes]
+    datas = [oracle.splitmix64_bytes(77 + i, L) for i, L in enumerate(sizes)]
+    per = [N * g.slice_len for g in geo]
+    objs = [(0, sizes[0], 0, 0), (sizes[0], sizes[1], per[0], 0)]
+    exp = b"".join(b"".join(oracle.slicer_encode(oracle.OracleClay(20, 7, 16), d.tobytes())) for d in datas)
+    h_in = batch.host_empty(sum(sizes))
+    h_in[:] = np.concatenate(datas)
+    h_out = batch.host_empty(sum(per))
+    batch.encode_batch_host(s, h_in, objs, h_out)
+    assert h_out.tobytes() == exp
+    del h_in, h_out  # freed by their finalizers
+    p_in = np.concatenate(datas)
+    p_out = np.zeros(sum(per), np.uint8)
+    batch.host_register(p_in)
+    batch.host_register(p_out)
+    try:
+        batch.encode_batch_host(s, p_in, objs, p_out)
+    finally:
+        batch.host_unregister(p_in)
+        batch.host_unregister(p_out)
+    assert p_out.tobytes() == exp

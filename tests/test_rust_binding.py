@@ -49,7 +49,7 @@ def test_shim_calls_every_coder_entry_point():
     shim = "".join(open(os.path.join(src_dir, f)).read() for f in sorted(os.listdir(src_dir)) if f.endswith(".rs"))
     called = set(re.findall(r"ffi::(te_\w+)\(", shim))
     wanted = {s for s in _lib.declared_symbols()
-              if re.match(r"te_(clay|slicer|stream)_|te_repair_plan_(from|free|get_info)|te_extract_repair_data", s)}
+              if re.match(r"te_(clay|slicer|stream)_|te_repair_plan_(from|free|get_info)|te_extract_repair_data|te_host_(alloc|free)$", s)}
     assert wanted <= called, sorted(wanted - called)
 
 
