@@ -128,7 +128,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--objects", type=int, default=1024, help="objects per GPU per step")
     ap.add_argument("--object-bytes", type=int, default=4 * MiB)
-    ap.add_argument("--mode", choices=["encode", "repair", "decode", "commit", "recover", "outer", "stream"],
+    ap.add_argument("--mode", choices=["encode", "repair", "decode", "commit", "recover", "outer", "stream", "percall"],
                     default="encode")
     ap.add_argument("--chunk-bytes", type=int, default=64 * MiB,
                     help="--mode stream: MAX_TRACK_SIZE, the SDK's stream chunk (sdk/src/stream/manifest.rs:22)")
@@ -173,6 +173,8 @@ def main():
         return outer_bench(args, torch, dist, world, rank, dev)
     if args.mode == "stream":
         return stream_bench(args, torch, dist, world, rank, dev)
+    if args.mode == "percall":
+        return percall_bench(args, torch, dist, world, rank, dev)
     L, nobj = args.object_bytes, args.objects
     slicer = T.Slicer.clay_default()
     g = slicer.geometry(L)
@@ -597,6 +599,105 @@ def stream_bench(args, torch, dist, world, rank, dev):
         dist.destroy_process_group()
 
 
+def percall_bench(args, torch, dist, world, rank, dev):
+    """--mode percall: the unchanged callers' shape.  lib/slicer's callers use one
+    object per call with pageable Vec<u8>s: Slicer::encode per track (sdk/src/track/write.rs:273-308,
+    objects <= 64 MiB), Slicer::repair per lost slice (network/node/src/features/spool/repair.rs:
+    312-339), Slicer::decode per read.  Times te_slicer_encode / te_slicer_decode (7 slices, the
+    worst case 13..19) / te_slicer_repair (lost 0, every other slice a helper) per call at 4 MiB and
+    64 MiB, with pageable buffers and with te_host_alloc'd ones, beside the oracle on one thread
+    (cpu_baseline; the reference itself is single-threaded per call).  Each output is checked."""
+    import ctypes as C
+    import numpy as np
+    import tape_amd as T
+    from tape_amd import batch
+    from tape_amd._lib import lib
+    s = T.Slicer.clay_default()
+    cfg, hdl = s._cfg(), s.coder.handle
+    ptr = lambda a: C.c_void_p(a.ctypes.data)
+    res, ok, cpu = {}, True, {}
+    for L in (4 * MiB, 64 * MiB):
+        g = s.geometry(L)
+        sl, per = g.slice_len, N * g.slice_len
+        d = torch.empty(L, dtype=torch.uint8, device=dev)
+        splitmix_fill(torch, d, 0, 1, L)
+        src = d.cpu().numpy()
+        avail = list(range(1, N))
+        plan = s.repair_plan_from_params(0, avail, L, g.stripe_size)
+        reps = 20 if L <= 4 * MiB else 5
+        for kind in ("pageable", "pinned"):
+            alloc = (lambda n: np.empty(n, np.uint8)) if kind == "pageable" else batch.host_empty
+            data, out, dec, rep = alloc(L), alloc(per), alloc(L), alloc(sl)
+            data[:] = src
+
+            def enc():
+                assert lib.te_slicer_encode(hdl, C.byref(cfg), ptr(data), L, ptr(out), per) == 0
+            enc()
+            ptrs = (C.c_void_p * N)()
+            for i in range(13, 20):
+                ptrs[i] = out.ctypes.data + i * sl
+            got = C.c_size_t()
+
+            def dcd():
+                assert lib.te_slicer_decode(hdl, C.byref(cfg), ptrs, sl, ptr(dec), L, C.byref(got)) == 0
+            blobs = [T.extract_repair_data(out[h * sl:(h + 1) * sl].tobytes(), plan, h) for h in avail]
+            hbuf = alloc(sum(len(b) for b in blobs))
+            hp, hl = (C.c_void_p * N)(), (C.c_size_t * N)()
+            at = 0
+            for h, b in zip(avail, blobs):
+                hbuf[at:at + len(b)] = np.frombuffer(b, np.uint8)
+                hp[h], hl[h] = hbuf.ctypes.data + at, len(b)
+                at += len(b)
+            meta = (C.c_uint8 * 48).from_buffer_copy(out[sl - 48:sl].tobytes())
+
+            def rpr():
+                assert lib.te_slicer_repair(hdl, plan.handle, hp, hl, meta, ptr(rep), sl) == 0
+            row = {}
+            for name, fn in (("encode", enc), ("decode", dcd), ("repair", rpr)):
+                fn()
+                t = time.perf_counter()
+                for _ in range(reps):
+                    fn()
+                ms = (time.perf_counter() - t) / reps * 1e3
+                row[name] = {"ms_per_call": round(ms, 3), "GiBps": round(L / ms / 1e3 / 2**30 * 1e3, 3)}
+            ok = ok and np.array_equal(dec, src) and np.array_equal(rep, out[:sl])
+            res[f"{L >> 20}MiB_{kind}"] = row
+        if rank == 0 and args.cpu_sample > 0:
+            cpu[f"{L >> 20}MiB"] = cpu_baseline_percall(src, out, sl, L, g.stripe_size)
+            ok = ok and cpu[f"{L >> 20}MiB"].pop("encode_equal")
+    if rank == 0:
+        print(json.dumps({
+            "metric": "per-call Slicer::encode / decode / repair ms, one object per call, host buffers, 1 MI355X",
+            "value": res["4MiB_pageable"]["encode"]["ms_per_call"], "unit": "ms", "n_gpus": world, "steps": None,
+            "warmup": 1, "ms_per_step": res["4MiB_pageable"]["encode"]["ms_per_call"], "higher_is_better": False,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (SplitMix64), host memory",
+            "config": {"workload": "te_slicer_encode / te_slicer_decode (slices 13..19) / te_slicer_repair (lost 0, "
+                                   "19 helpers), one object per call, 4 MiB and 64 MiB", "profile": "clay(20,7,16)"},
+            "calls": res, "roofline": None, "cpu_baseline": cpu, "outputs_verified": bool(ok)}), flush=True)
+
+
+def cpu_baseline_percall(src, out, sl, L, stripe):
+    """The oracle (C restatement of lib/slicer) per call on one thread: encode, decode from the same
+    7 slices, repair of slice 0 from the other 19 (kind "port")."""
+    from oracle import oracle as O
+    clay = O.OracleClay(20, 7, 16)
+    t = time.perf_counter()
+    exp = O.slicer_encode_np(clay, src)
+    te = time.perf_counter() - t
+    slices = {i: out[i * sl:(i + 1) * sl].tobytes() for i in range(13, 20)}
+    t = time.perf_counter()
+    O.slicer_decode(clay, slices)
+    td = time.perf_counter() - t
+    cs, stripes = O.repair_plan(clay, 0, list(range(1, N)), L, stripe)
+    helpers = {h: O.extract_repair_data(out[h * sl:(h + 1) * sl].tobytes(), cs, clay.alpha, stripes, h)
+               for h in range(1, N)}
+    t = time.perf_counter()
+    O.slicer_repair(clay, cs, stripes, helpers, out[sl - 48:sl].tobytes())
+    tr = time.perf_counter() - t
+    return {"encode_ms": round(te * 1e3, 2), "decode_ms": round(td * 1e3, 2), "repair_ms": round(tr * 1e3, 2),
+            "cores": 1, "kind": "port", "encode_equal": bool((exp.reshape(-1) == out).all())}
+
+
 def cpu_baseline_stream(args, r, CB, R):
     """The reference's stream encode on host cores: per chunk the oracle's Slicer::encode (C
     restatement, AVX2 region multiply) + hashlib SHA-256 leaves + merkle root and proofs (the
@@ -793,16 +894,25 @@ def cpu_baseline(args, np, torch, d_in, d_out, per, L):
     wall = time.perf_counter() - t
     gpu = d_out[:m * per].cpu().numpy()
     match = bool(np.array_equal(gpu, out))
-    one = host_in[:L]
+    # the same code path on one thread (the single-thread figure came from
+    # another entry point), over >= 8 objects
+    m1 = min(m, 16)
     t = time.perf_counter()
-    O.slicer_encode_np(clay, one)
-    single = time.perf_counter() - t
+    O.encode_many(clay, host_in, L, m1, out, per, 1)
+    single = m1 * L / (time.perf_counter() - t) / 2**30
+    # and on every core this process may use (the whole host, not the GPU's 16-core share)
+    all_cores = None
+    if cores > thr:
+        t = time.perf_counter()
+        O.encode_many(clay, host_in, L, m, out, per, cores)
+        all_cores = round(m * L / (time.perf_counter() - t) / 2**30, 4)
     return {"value": round(m * L / wall / 2**30, 4), "unit": "GiB/s", "cores": thr, "kind": "port",
             "sample": f"{m} x 4 MiB objects (first {m} of the batch), {thr} threads, one object per thread; "
                       "oracle/clay_oracle.c: the Clay layering restated in C over an AVX2 nibble-shuffle GF(2^8) "
                       "region multiply -- the method of reed-solomon-erasure's simd-accel C kernel, which the "
                       "reference's Cargo.lock enables (cc + libc resolved)",
-            "single_thread_GiBps": round(L / single / 2**30, 4), "affinity_cores": cores,
+            "single_thread_GiBps": round(single, 4), "single_thread_objects": m1,
+            "all_affinity_cores_GiBps": all_cores, "affinity_cores": cores,
             "gpu_matches_oracle_on_sample": match}
 
 

@@ -112,6 +112,12 @@ int te_clay_set_decode_jit(te_clay *c, int mode, uint64_t min_stripes);
 /* Pattern kernels ready / compiling / failed on the handle, after waiting up to `timeout_ms` for
  * compiles in flight to finish. */
 int te_clay_decode_jit_status(te_clay *c, uint32_t timeout_ms, uint32_t *ready, uint32_t *pending, uint32_t *failed);
+/* The handle's device-resident decode pattern store (diagnostics): slots allocated (it grows by
+ * doubling from 256 to 8192, ~26 KB of device memory each) and filled, how often a full store was
+ * emptied, how often it grew, and how many calls had more distinct stripe patterns than it holds
+ * (those upload their patterns with the call instead). */
+int te_clay_decode_store_stats(te_clay *c, uint32_t *capacity, uint32_t *used, uint64_t *clears, uint64_t *grows,
+                               uint64_t *arena_calls);
 int te_clay_get_info(const te_clay *c, te_clay_info *out);
 /* ClayCoder::chunk_size_for  clay.rs:61-73 */
 size_t te_clay_chunk_size_for(const te_clay *c, size_t input_len);

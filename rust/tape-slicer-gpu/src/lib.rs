@@ -200,6 +200,13 @@ impl ClayCoder {
         if s != 0 { fatal(s) }
         (r, p, f)
     }
+    /// The device decode-pattern store: (capacity, filled, clears, grows, over-capacity calls).
+    pub fn decode_store_stats(&self) -> (u32, u32, u64, u64, u64) {
+        let (mut cap, mut used, mut cl, mut gr, mut ar) = (0u32, 0u32, 0u64, 0u64, 0u64);
+        let s = unsafe { ffi::te_clay_decode_store_stats(self.raw.as_ptr(), &mut cap, &mut used, &mut cl, &mut gr, &mut ar) };
+        if s != 0 { fatal(s) }
+        (cap, used, cl, gr, ar)
+    }
 }
 
 impl ErasureCoder for ClayCoder {

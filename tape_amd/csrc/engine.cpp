@@ -278,14 +278,22 @@ struct te_clay {
     // sets make nearly every stripe a pattern of its own, and re-uploading ~26 KB per stripe per
     // call cost more host time than the kernel takes.  Slots are handed out in order; a full store
     // is emptied after its last reader (`used`) has finished.
+    // The store grows by doubling from kMin slots (each slot ~26 KB of device memory: 102 steps
+    // of DecStepP plus its GpePattern and header; kCap slots = ~215 MB) once its last reader is
+    // done.  New slots are filled with stream-ordered copies from the call's descriptor upload
+    // (decode_enqueue), never with a host-blocking copy; a call on another stream waits for the
+    // last fill (`written`) before reading.
     struct DecStore {
-        static constexpr uint32_t kCap = 8192;
+        static constexpr uint32_t kCap = 8192, kMin = 256;
         static constexpr uint32_t kSteps = kRepQ * kRepQ + 2;  // 100 planes + 2 blank steps
         DevBuf pats, hdrs, steps, soff;
+        uint32_t cap = 0;
         std::unordered_map<uint64_t, uint32_t> slot;
         uint32_t n = 0;
-        hipEvent_t used = nullptr;
-        bool used_pending = false;
+        hipEvent_t used = nullptr, written = nullptr;
+        bool used_pending = false, written_pending = false;
+        hipStream_t written_stream = nullptr;
+        uint64_t clears = 0, grows = 0, arena_calls = 0;  // te_clay_decode_store_stats
     } dstore;
     // per-pattern decode kernels built at run time (dec_rtc.cpp); created on first decode
     DecJit *jit = nullptr;
@@ -346,8 +354,11 @@ static void release_device_state(te_clay *c) {
     c->dstore.slot.clear();
     c->dstore.n = 0;
     if (c->dstore.used) (void)hipEventDestroy(c->dstore.used);
-    c->dstore.used = nullptr;
-    c->dstore.used_pending = false;
+    if (c->dstore.written) (void)hipEventDestroy(c->dstore.written);
+    c->dstore.used = c->dstore.written = nullptr;
+    c->dstore.used_pending = c->dstore.written_pending = false;
+    c->dstore.written_stream = nullptr;
+    c->dstore.cap = 0;
     if (c->rec_done) (void)hipEventDestroy(c->rec_done);
     c->rec_done = nullptr;
     dec_jit_free(c->jit);  // joins compiles in flight; every stream is drained above
@@ -499,6 +510,18 @@ int te_clay_set_decode_jit(te_clay *c, int mode, uint64_t min_stripes) {
     c->jit_mode = mode;
     c->jit_min = min_stripes;
     if (c->jit) dec_jit_set(c->jit, mode, min_stripes);
+    return TE_OK;
+}
+
+int te_clay_decode_store_stats(te_clay *c, uint32_t *capacity, uint32_t *used, uint64_t *clears, uint64_t *grows,
+                               uint64_t *arena_calls) {
+    if (!c) return TE_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (capacity) *capacity = c->dstore.cap;
+    if (used) *used = c->dstore.n;
+    if (clears) *clears = c->dstore.clears;
+    if (grows) *grows = c->dstore.grows;
+    if (arena_calls) *arena_calls = c->dstore.arena_calls;
     return TE_OK;
 }
 
@@ -924,38 +947,65 @@ void dec_precompile(te_clay *c, const std::vector<std::pair<uint64_t, int>> &key
 }
 
 // Slots of the device-resident pattern store (te_clay::DecStore) for the staged patterns of one
-// call, uploading the ones not there yet.  false: more distinct patterns than the store holds
-// (the call then uploads its patterns through the arena).
+// call.  The patterns not there yet are appended to U (host images of their store entries) for
+// decode_enqueue to upload with the call's descriptors and copy into their slots on the call's
+// stream.  false: more distinct patterns than the store holds (the call then uploads its patterns
+// through the arena).
+struct StoreFill {
+    uint32_t n0 = 0;                  // first new slot
+    bool wait_used = false;           // new slots overwrite slots earlier launches may still read
+    std::vector<GpePattern> pats;
+    std::vector<DecProgHdr> hdrs;
+    std::vector<DecStepP> steps;
+    std::vector<uint32_t> soff;       // slot -> step offset, when the store was (re)allocated
+};
 bool dec_store_slots(te_clay *c, const std::vector<const te_clay::DecCache *> &cached, const std::vector<uint64_t> &keys,
-                     std::vector<uint32_t> &slot_of, int &rc) {
+                     std::vector<uint32_t> &slot_of, StoreFill &U, int &rc) {
     te_clay::DecStore &S = c->dstore;
     constexpr uint32_t kCap = te_clay::DecStore::kCap, kSteps = te_clay::DecStore::kSteps;
     rc = TE_OK;
-    if (keys.size() > kCap) return false;
-    if (!S.pats.p) {
-        if ((rc = hip_status(S.pats.ensure((size_t)kCap * sizeof(GpePattern))))) return false;
-        if ((rc = hip_status(S.hdrs.ensure((size_t)kCap * sizeof(DecProgHdr))))) return false;
-        if ((rc = hip_status(S.steps.ensure((size_t)kCap * kSteps * sizeof(DecStepP))))) return false;
-        if ((rc = hip_status(S.soff.ensure((size_t)kCap * sizeof(uint32_t))))) return false;
-        std::vector<uint32_t> so(kCap);
-        for (uint32_t i = 0; i < kCap; i++) so[i] = i * kSteps;
-        if ((rc = hip_status(hipMemcpy(S.soff.p, so.data(), so.size() * sizeof(uint32_t), hipMemcpyHostToDevice)))) return false;
+    if (keys.size() > kCap) {
+        S.arena_calls++;
+        return false;
+    }
+    if (!S.used) {
         if ((rc = hip_status(hipEventCreateWithFlags(&S.used, hipEventDisableTiming)))) return false;
-        S.slot.clear();
-        S.n = 0;
+        if ((rc = hip_status(hipEventCreateWithFlags(&S.written, hipEventDisableTiming)))) return false;
     }
     size_t fresh = 0;
     for (uint64_t k : keys) fresh += S.slot.count(k) == 0;
-    if (S.n + fresh > kCap) {  // full: empty it once its last reader is done
-        if (S.used_pending && (rc = hip_status(hipEventSynchronize(S.used)))) return false;
+    if (S.n + fresh > S.cap) {
+        // grow (doubling, up to kCap) when the call's patterns do not fit, else empty the full
+        // store; either way the old contents go once their last reader is done
+        const uint32_t need = (uint32_t)std::min<size_t>(kCap, std::max<size_t>(keys.size(), (size_t)S.n + fresh));
+        if (S.cap < kCap && need > S.cap) {
+            uint32_t cap = std::max(te_clay::DecStore::kMin, S.cap);
+            while (cap < need) cap *= 2;
+            cap = std::min(cap, kCap);
+            // the buffers are freed: every launch that read them must be done (rare: <= 6 times)
+            if (S.used_pending && (rc = hip_status(hipEventSynchronize(S.used)))) return false;
+            S.used_pending = false;
+            S.pats.release();
+            S.hdrs.release();
+            S.steps.release();
+            S.soff.release();
+            if ((rc = hip_status(S.pats.ensure((size_t)cap * sizeof(GpePattern))))) return false;
+            if ((rc = hip_status(S.hdrs.ensure((size_t)cap * sizeof(DecProgHdr))))) return false;
+            if ((rc = hip_status(S.steps.ensure((size_t)cap * kSteps * sizeof(DecStepP))))) return false;
+            if ((rc = hip_status(S.soff.ensure((size_t)cap * sizeof(uint32_t))))) return false;
+            S.cap = cap;
+            U.soff.resize(cap);
+            for (uint32_t i = 0; i < cap; i++) U.soff[i] = i * kSteps;
+            S.grows++;
+        } else {
+            U.wait_used = S.used_pending;  // the fill waits (on the device) for the last reader
+            S.clears++;
+        }
         S.slot.clear();
         S.n = 0;
     }
     slot_of.assign(keys.size(), 0);
-    const uint32_t n0 = S.n;
-    std::vector<GpePattern> np;
-    std::vector<DecProgHdr> nh;
-    std::vector<DecStepP> ns;
+    U.n0 = S.n;
     for (size_t i = 0; i < keys.size(); i++) {
         auto f = S.slot.find(keys[i]);
         if (f != S.slot.end()) {
@@ -965,18 +1015,9 @@ bool dec_store_slots(te_clay *c, const std::vector<const te_clay::DecCache *> &c
         const uint32_t sl = S.n++;
         S.slot.emplace(keys[i], sl);
         slot_of[i] = sl;
-        np.push_back(cached[i]->P);
-        nh.push_back(cached[i]->H);
-        ns.insert(ns.end(), cached[i]->steps.begin(), cached[i]->steps.end());
-    }
-    if (!np.empty()) {  // new slots are [n0, n): three copies (synchronous: cold patterns only)
-        if ((rc = hip_status(hipMemcpy(S.pats.as<GpePattern>() + n0, np.data(), np.size() * sizeof(GpePattern),
-                                       hipMemcpyHostToDevice))) ||
-            (rc = hip_status(hipMemcpy(S.hdrs.as<DecProgHdr>() + n0, nh.data(), nh.size() * sizeof(DecProgHdr),
-                                       hipMemcpyHostToDevice))) ||
-            (rc = hip_status(hipMemcpy(S.steps.as<DecStepP>() + (size_t)n0 * kSteps, ns.data(), ns.size() * sizeof(DecStepP),
-                                       hipMemcpyHostToDevice))))
-            return false;
+        U.pats.push_back(cached[i]->P);
+        U.hdrs.push_back(cached[i]->H);
+        U.steps.insert(U.steps.end(), cached[i]->steps.begin(), cached[i]->steps.end());
     }
     return true;
 }
@@ -1126,12 +1167,13 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     // staged patterns live in the device store (uploaded once per handle), the jobs name slots;
     // otherwise (generic kernel, or more patterns than the store holds) they go in the arena
     std::vector<uint32_t> slot_of;
+    StoreFill fill;
     bool in_store = false;
     bool every_group_staged = staged;  // the generic kernel reads per-call patterns (plane lists)
     for (auto &kv : groups) every_group_staged = every_group_staged && (kv.second.empty() || staged_group(kv.first));
     if (every_group_staged) {
         int rs = TE_OK;
-        in_store = dec_store_slots(c, cached, pat_keys, slot_of, rs);
+        in_store = dec_store_slots(c, cached, pat_keys, slot_of, fill, rs);
         if (rs) return rs;
         if (in_store)
             for (auto &kv : groups)
@@ -1167,8 +1209,40 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     for (auto &kv : groups)
         if (!kv.second.empty()) offs.push_back({kv.first, A.put(kv.second.data(), kv.second.size() * sizeof(GpeJob))});
     for (Fixed &f : fixed) f.off = A.put(f.jobs.data(), f.jobs.size() * sizeof(GpeJob));
+    // new store entries ride in the same upload, then move to their slots on this stream
+    size_t fp_off = 0, fh_off = 0, fs_off = 0, fo_off = 0;
+    if (in_store && !fill.pats.empty()) {
+        fp_off = A.put(fill.pats.data(), fill.pats.size() * sizeof(GpePattern));
+        fh_off = A.put(fill.hdrs.data(), fill.hdrs.size() * sizeof(DecProgHdr));
+        fs_off = A.put(fill.steps.data(), fill.steps.size() * sizeof(DecStepP), 64);
+    }
+    if (in_store && !fill.soff.empty()) fo_off = A.put(fill.soff.data(), fill.soff.size() * sizeof(uint32_t));
     int r = A.upload(s);
     if (r) return r;
+    if (in_store) {
+        te_clay::DecStore &S = c->dstore;
+        if (fill.wait_used) TE_HIP(hipStreamWaitEvent(s, S.used, 0));
+        // entries another stream filled and nobody on this stream has waited for yet
+        if (S.written_pending && S.written_stream != s) TE_HIP(hipStreamWaitEvent(s, S.written, 0));
+        const bool any = !fill.pats.empty() || !fill.soff.empty();
+        if (!fill.pats.empty()) {
+            const size_t np = fill.pats.size();
+            TE_HIP(hipMemcpyAsync(S.pats.as<GpePattern>() + fill.n0, A.at<GpePattern>(fp_off), np * sizeof(GpePattern),
+                                  hipMemcpyDeviceToDevice, s));
+            TE_HIP(hipMemcpyAsync(S.hdrs.as<DecProgHdr>() + fill.n0, A.at<DecProgHdr>(fh_off), np * sizeof(DecProgHdr),
+                                  hipMemcpyDeviceToDevice, s));
+            TE_HIP(hipMemcpyAsync(S.steps.as<DecStepP>() + (size_t)fill.n0 * te_clay::DecStore::kSteps,
+                                  A.at<DecStepP>(fs_off), fill.steps.size() * sizeof(DecStepP), hipMemcpyDeviceToDevice, s));
+        }
+        if (!fill.soff.empty())
+            TE_HIP(hipMemcpyAsync(S.soff.p, A.at<uint32_t>(fo_off), fill.soff.size() * sizeof(uint32_t),
+                                  hipMemcpyDeviceToDevice, s));
+        if (any) {
+            TE_HIP(hipEventRecord(S.written, s));
+            S.written_pending = true;
+            S.written_stream = s;
+        }
+    }
     auto dec_args = [&](const std::pair<uint64_t, size_t> &o) {
         const uint64_t cs = o.first >> 32;
         const uint32_t sc = (uint32_t)(cs / (uint64_t)h.alpha);

@@ -283,6 +283,16 @@ class ClayCoder:
         if r:
             raise _engine_error(r)
 
+    def decode_store_stats(self) -> dict:
+        """te_clay_decode_store_stats: the device pattern store's capacity, filled slots, clears,
+        grows and over-capacity (arena) calls."""
+        cap, used = C.c_uint32(), C.c_uint32()
+        cl, gr, ar = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(lib.te_clay_decode_store_stats(self.handle, C.byref(cap), C.byref(used), C.byref(cl), C.byref(gr),
+                                              C.byref(ar)), "decode")
+        return {"capacity": cap.value, "used": used.value, "clears": cl.value, "grows": gr.value,
+                "arena_calls": ar.value}
+
     def decode_jit_status(self, timeout_ms: int = 0) -> tuple:
         """(ready, compiling, failed) per-pattern kernels, after waiting up to timeout_ms."""
         v = [C.c_uint32(0) for _ in range(3)]
