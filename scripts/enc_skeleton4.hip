@@ -42,7 +42,8 @@ __device__ __forceinline__ void bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_
 
 // SYS: 0 = loader copies systematic pieces global -> global, 1 = row stores from the ring per plane
 // NB: transposition batches per row (nodes per batch = ceil(13 / NB))
-template <int SYS, int NB>
+// V: extra VALU per lane per plane (the encode's arithmetic is ~540 VALU per wave per plane)
+template <int SYS, int NB, int V = 0>
 __global__ void __launch_bounds__((G + 1) * 64, 1) skel(const uint8_t *in, uint8_t *out, uint32_t *sink) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint8_t *lds8 = reinterpret_cast<uint8_t *>(lds);
@@ -113,6 +114,9 @@ __global__ void __launch_bounds__((G + 1) * 64, 1) skel(const uint8_t *in, uint8
 #pragma unroll
             for (int r = 0; r < 16; r++) x[r] = *reinterpret_cast<const uint32_t *>(img + r * RW);
 #pragma unroll
+            for (int i = 0; i < V / 2; i++)
+                x[i & 15] = __builtin_amdgcn_bitop3_b32(x[i & 15], x[(i + 5) & 15] << 1, x[(i + 9) & 15], 0x96);
+#pragma unroll
             for (int n = 0; n < 13; n++) o[n][s] = x[n] ^ x[(n + 3) & 15] ^ (x[(n + 7) & 15] << 1);
             if (SYS == 1) {
                 // each wave stores ~1.2 of the 7 own rows from the ring image (2 b128 per row)
@@ -174,9 +178,9 @@ float timeit(F f, int reps) {
     return best;
 }
 
-template <int SYS, int NB>
+template <int SYS, int NB, int V = 0>
 void run(const char *name, uint8_t *din, uint8_t *dout, uint32_t *sink) {
-    auto fn = skel<SYS, NB>;
+    auto fn = skel<SYS, NB, V>;
     constexpr int PER = (13 + NB - 1) / NB;
     const size_t lds = 2 * SLOT + PER * TP;
     CK(hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -200,5 +204,8 @@ int main() {
     run<1, 2>("R10: sys row stores, 2 batches", din, dout, sink);
     run<0, 3>("R10: sys loader pieces, 3 batches", din, dout, sink);
     run<0, 2>("R10: sys loader pieces, 2 batches again", din, dout, sink);
+    run<0, 2, 300>("R10: + 300 VALU per plane", din, dout, sink);
+    run<0, 2, 540>("R10: + 540 VALU per plane", din, dout, sink);
+    run<0, 2, 800>("R10: + 800 VALU per plane", din, dout, sink);
     return 0;
 }

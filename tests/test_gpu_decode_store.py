@@ -109,6 +109,7 @@ def test_decode_store_two_streams():
     o1 = torch.zeros(nobj * L, dtype=torch.uint8, device="cuda")
     o2 = torch.zeros(nobj * L, dtype=torch.uint8, device="cuda")
     objs = [(i * per, g.slice_len, masks[i], i * L) for i in range(nobj)]
+    torch.cuda.synchronize()  # the zero fills above ran on the default stream
     batch.decode_batch(s, d_out, objs, meta * nobj, o1, s1)  # fills the store on s1
     batch.decode_batch(s, d_out, objs, meta * nobj, o2, s2)  # same patterns, read on s2
     torch.cuda.synchronize()
