@@ -2,7 +2,7 @@
 // Times enc_stage_kernel<7> over a device-resident 1024 x 4 MiB batch and
 // times each with hipEvents.  hipcc --offload-arch=gfx950 -O3 -std=c++20 -I tape_amd/csrc
 #include "../tape_amd/csrc/encode_stage.hip"
-#include "../tape_amd/csrc/encode_dma.hip"
+#include "kbench_encode_dma.hip"
 #include <cstdio>
 #include <vector>
 #include <map>

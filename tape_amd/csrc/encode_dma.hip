@@ -1,27 +1,23 @@
-// encode_dma.hip -- Clay(20,7,16) layered encode of 1 MB stripes (sub-chunk 1,281..1,440 bytes:
-// Slicer::encode of every object of 1 MB < L <= 100 MB, lib/slicer/src/adaptive.rs:31-39), the
-// production hot path.  Replaces ClayCoder::encode -> clay_codes::ClayCode::encode
+// encode_dma.hip -- Clay(20,7,16) layered encode of 1 MB stripes (sub-chunk 1,281..1,440 bytes),
+// row by row per plane.  Replaces ClayCoder::encode -> clay_codes::ClayCode::encode
 // (lib/slicer/src/clay.rs:99-104) in Slicer::encode's stripe loop (slicer.rs:268-286), fused
-// with distribute_chunks' rotation (slicer.rs:60-71).  Same algebra and plane order as
-// encode_stage.hip; what differs is how bytes move.
-//
-// Why a second kernel: encode_stage.hip loads every input word with its own 4-byte-per-lane
-// load (17 per wave per plane, half of them 2-aligned).  The TA spends the same ~16 cycles on a
-// dword wave-load as on a 16-byte one (PMC: TA_BUFFER_TOTAL_CYCLES / wavefronts), so its loads
-// alone keep the TA half busy.  Here:
+// with distribute_chunks' rotation (slicer.rs:60-71).  Since r04 the production kernel for the
+// common case is encode_r10.hip (row-of-planes pieces); this one serves the stripes that kernel
+// leaves: objects at 2-mod-4 offsets, a data end inside a dword (MASKED), chunk filters
+// (te_recover_batch_device's re-encode), other sub-chunk sizes.  Same algebra and plane order as
+// encode_stage.hip; what differs is how bytes move:
 //   * inputs arrive by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per wave-instruction, from
 //     2-aligned addresses -- scripts/ldsdma_probe.hip) into a two-slot ring of plane images,
-//     one plane ahead: 23 wave-instructions per plane instead of 102;
+//     one plane ahead, issued by a dedicated loader wave: 23 wave-instructions per plane;
 //   * the compute lanes (4 byte-columns each) read their words from the image (ds_read_b32);
 //   * column-1 pairs are parked in VGPRs (25 slots, compile-time indices via a switch on the
 //     plane digit), not in LDS; level-2 column-0 pairs park their U in the output slice at the
 //     place the pair's final C overwrites later, and are read back by the same DMA as the
 //     level-1 parity rows -- no scratch buffer;
 //   * systematic rows are written from the ring image (no staging copy);
-//   * the main loop holds no ordinary global load, so the compiler inserts no vmcnt waits: the
-//     DMA is issued from inline asm and waited for explicitly before the barrier that frees
-//     the ring slot.
-// LDS: 2 x 23,552 B ring + 24 x 1,440 B staging = 81,664 B -> two workgroups (12 waves) per CU.
+//   * the compute waves issue no loads, so the compiler inserts no vmcnt waits for them: the
+//     loader waits for its DMA explicitly before the barrier that hands the plane over.
+// LDS: 2 x 23,552 B ring + 24 x 1,440 B staging = 81,664 B -> two workgroups (14 waves) per CU.
 #include "kernels.hpp"
 #include "gf_dev.hpp"
 #include "dev_io.hpp"
@@ -40,73 +36,22 @@ constexpr uint32_t kOwnBlk = 7 * RB;       // 7 own rows, then 9 partner rows; t
 constexpr uint32_t kPartBlk = 9 * RB;      // overhang a region run with those lanes masked off
 constexpr uint32_t kPartBase = kOwnBlk * 16;
 constexpr uint32_t kSlotBytes = (kOwnBlk + kPartBlk) * 16;
-#ifndef TEC_DMA_DIRECT
-#define TEC_DMA_DIRECT 0  // 1 (timing builds): no staging -- each compute lane stores its word of every output row
-#endif                    // itself (one barrier per plane, a three-slot ring): 5.70 against 5.03 ms, row
-                          // pieces split between waves store slowly (skeleton: 5.86 against 4.43 ms)
-constexpr uint32_t kRing = TEC_DMA_DIRECT ? 3 : 2;   // ring slots (planes in flight)
+constexpr uint32_t kRing = 2;              // ring slots (planes in flight)
 constexpr uint32_t kStageBase = kRing * kSlotBytes;
-#ifndef TEC_DMA_STAGE_ROWS
-#define TEC_DMA_STAGE_ROWS 24
-#endif
-constexpr uint32_t kStageRows = TEC_DMA_STAGE_ROWS;  // < 24: timing builds only
-constexpr uint32_t kLdsBytes = kStageBase + (TEC_DMA_DIRECT ? 0u : kStageRows * RW);
+constexpr uint32_t kStageRows = 24;
+constexpr uint32_t kLdsBytes = kStageBase + kStageRows * RW;
 static_assert(kLdsBytes <= 81920 - 1024, "two workgroups per CU, with a margin");
-#ifndef TEC_DMA_LDS_PAD
-#define TEC_DMA_LDS_PAD 0  // timing builds only: extra LDS requested (occupancy probes)
-#endif
-constexpr uint32_t kLdsLaunch = kLdsBytes + TEC_DMA_LDS_PAD;
-#ifndef TEC_DMA_LOADER
-#define TEC_DMA_LOADER 1  // 1: a seventh wave issues every DMA; the six compute waves only store
-#endif
 constexpr int kOwnInstr = 10, kPartInstr = 13, kDmaInstr = kOwnInstr + kPartInstr;
-constexpr int kDmaWaves = TEC_DMA_LOADER ? 1 : G;   // waves that issue DMA
-constexpr int kDmaPerWave = (kDmaInstr + kDmaWaves - 1) / kDmaWaves;  // 23 (loader) or 4
-constexpr int kWaves = G + (TEC_DMA_LOADER ? 1 : 0);
+constexpr int kWaves = G + 1;              // six compute waves and a loader wave that issues every DMA
 // compute waves keep at most this many stores in flight before B1, so every slice row a
 // later DMA reads back (level-2 partners, >= 8 steps later) has landed: <= 3 steps of stores
 constexpr int kCap = 5;  // flush rows per wave per step
-#ifndef TEC_DMA_LAG
-#define TEC_DMA_LAG 30
-#endif
-constexpr int kStoreLag = TEC_DMA_LAG;
-// DIRECT: a compute wave issues 11..32 word stores per plane (+ 16-bit tail stores in one wave)
-constexpr int kDirectLag = 48;
+constexpr int kStoreLag = 30;
 static_assert(kStoreLag <= 3 * 2 * kCap && kStoreLag < 64, "stores older than 3 steps must have landed");
 constexpr uint32_t kDrop = 0x80000000u;    // offset past every resource: the range check drops it
-#ifndef TEC_DMA_PRIO
-#define TEC_DMA_PRIO 0    // wave priority during a plane's compute (s_setprio)
-#endif
-#ifndef TEC_DMA_L2NT
-#define TEC_DMA_L2NT 1    // level-2 partner rows (read back from the slices) with nt
-#endif
-#ifndef TEC_DMA_ST_AUX
-#define TEC_DMA_ST_AUX 2  // slice stores: 2 = nt, 0 = default
-#endif
-#ifndef TEC_DMA_ORDER
-#define TEC_DMA_ORDER 1   // 1: a step's stores are issued before the next plane's DMA (B1 waits vmcnt(0));
-                          // 0: DMA first, B1 waits vmcnt(2) (measured 3 % slower);
-                          // 2: DMA first, B1 waits only for it: the previous step's stores stay in flight
-#endif
-#ifndef TEC_DMA_SLP
-#define TEC_DMA_SLP 1     // MDS as the shared-XOR program (mds_slp.inc); 0: row by row (timing builds)
-#endif
-#ifndef TEC_DMA_WPE
-#define TEC_DMA_WPE 4     // waves per SIMD the register budget is cut for (4: <= 128 VGPRs)
-#endif
-#ifndef TEC_DMA_KPRIO
-#define TEC_DMA_KPRIO 0   // wave priority of the whole kernel (s_setprio; 2 measured 6 % slower alone)
-#endif
-#ifndef TEC_DMA_LPRIO
-#define TEC_DMA_LPRIO 0   // loader wave priority (s_setprio)
-#endif
-#ifndef TEC_DMA_STORE_MASK
-#define TEC_DMA_STORE_MASK 1  // per-job chunk filter (te_recover_batch_device); 0: timing builds only
-#endif
-#ifndef TEC_DMA_ABLATE
-#define TEC_DMA_ABLATE 0  // timing builds only (scripts/kbench.hip): bit0 no stores, bit1 no DMA,
-#endif                    // bit2 trivial MDS, bit3 no vmcnt wait at B1, bit4 no B2 barrier,
-                          // bit6 no partner DMA, bit7 no level-2 partner DMA
+constexpr int kStAux = 2;                  // slice stores: nt
+// (r01-r03 timing variants of this kernel -- direct stores, DMA orders, priorities, ablations,
+// occupancy probes -- live in the measurement copy scripts/kbench_encode_dma.hip)
 
 // Staging rows (per plane).
 constexpr int kRowC0 = 0;   // 0..2: node 7+r at this plane (level 1 parity; level 2 red / pair / park)
@@ -238,14 +183,10 @@ __device__ __forceinline__ void col1(const uint32_t *u1, uint32_t (&sl)[kSlots],
 
 // MASKED: the stripe's data end is not dword aligned (an object's last stripe only).
 template <bool MASKED>
-__global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncArgs a) {
+__global__ void __launch_bounds__(kWaves * 64, 4) enc_dma_kernel(EncArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint8_t *const lds8 = reinterpret_cast<uint8_t *>(lds);
     const uint32_t lds0 = __builtin_amdgcn_groupstaticsize();  // LDS address of the dynamic array
-    // above the commitment kernel's waves: te_encode_commit_batch_host hashes one group while the
-    // next one encodes, and a leaf wave sharing a SIMD would otherwise halve the encode there
-    // (a copy window's D2H waits for its encode)
-    if constexpr (TEC_DMA_KPRIO) __builtin_amdgcn_s_setprio(TEC_DMA_KPRIO);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
 
@@ -291,20 +232,19 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
     }
     asm volatile("s_waitcnt vmcnt(0)" ::"v"(fixw) : "memory");
 
-    // DMA pieces of this wave: instruction i = wv + 6k of the 23 per plane (0..9 own rows,
-    // 10..22 partner rows).  dvo = per-lane source offset (partner: for x = p; +10 sc when the
-    // piece's partner row index p >= z0 skips the red node), dp = partner row index.
-    uint32_t dvo[kDmaPerWave];
+    // DMA pieces of the loader wave: instruction i of the 23 per plane (0..9 own rows, 10..22
+    // partner rows).  dvo = per-lane source offset (partner: for x = p; +10 sc when the piece's
+    // partner row index p >= z0 skips the red node).
+    uint32_t dvo[kDmaInstr];
 #pragma unroll
-    for (int k = 0; k < kDmaPerWave; k++) {
-        const uint32_t i = (TEC_DMA_LOADER ? 0u : wv) + (uint32_t)(kDmaWaves * k);
-        dvo[k] = kDrop;
-        if (i < (uint32_t)kOwnInstr) {
+    for (int i = 0; i < kDmaInstr; i++) {
+        dvo[i] = kDrop;
+        if (i < kOwnInstr) {
             const uint32_t b = 64u * i + lane, x = b / RB, j = b - x * RB;
-            if (b < (uint32_t)K * RB) dvo[k] = x * cs + 16u * j;
+            if (b < (uint32_t)K * RB) dvo[i] = x * cs + 16u * j;
         } else {
             const uint32_t b = 64u * (i - kOwnInstr) + lane, p = b / RB, j = b - p * RB;
-            if (b < 9u * RB) dvo[k] = p * kQ * sc + 16u * j;  // 16 j < 10 sc: p >= z0 <=> dvo >= 10 sc z0
+            if (b < 9u * RB) dvo[i] = p * kQ * sc + 16u * j;  // 16 j < 10 sc: p >= z0 <=> dvo >= 10 sc z0
         }
     }
     // DMA of plane tp into ring slot `slot`: own rows from the input; partner rows C(z0, (x, s)),
@@ -318,24 +258,17 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
         const uint32_t so_part = __builtin_amdgcn_readfirstlane(lvl2 ? slice_off(nz0) + ns * sc : src_al + nz0 * cs + ns * sc);
         const uint32_t skip = kQ * sc, skip_from = skip * nz0;
 #pragma unroll
-        for (int k = 0; k < kDmaPerWave; k++) {
-            const uint32_t i = (TEC_DMA_LOADER ? 0u : wv) + (uint32_t)(kDmaWaves * k);
-            if (i >= (uint32_t)kDmaInstr || (TEC_DMA_ABLATE & 2)) continue;
+        for (int i = 0; i < kDmaInstr; i++) {
             // lanes past the region's last block are masked off (an LDS-DMA lane that is merely
             // range-dropped still writes zeros to its LDS destination)
-            if (i < (uint32_t)kOwnInstr) {
-                const uint32_t ld = __builtin_amdgcn_readfirstlane(lds0 + slot + 1024u * i);
-                if (dvo[k] != kDrop) dma16<false>(rs_src, dvo[k], so_own, ld);
+            if (dvo[i] == kDrop) continue;
+            if (i < kOwnInstr) {
+                dma16<false>(rs_src, dvo[i], so_own, __builtin_amdgcn_readfirstlane(lds0 + slot + 1024u * i));
             } else {
-                if ((TEC_DMA_ABLATE & 64) || ((TEC_DMA_ABLATE & 128) && lvl2)) continue;
-                const uint32_t vo = dvo[k] + (dvo[k] >= skip_from ? skip : 0u);
+                const uint32_t vo = dvo[i] + (dvo[i] >= skip_from ? skip : 0u);
                 const uint32_t ld = __builtin_amdgcn_readfirstlane(lds0 + slot + kPartBase + 1024u * (i - kOwnInstr));
-                if (dvo[k] != kDrop) {
-                    if ((TEC_DMA_ABLATE & 32) && lvl2) dma16<false>(rs_src, vo, so_own, ld);  // timing: no read-back
-                    else if (lvl2 && TEC_DMA_L2NT) dma16<true>(rs_dst, vo, so_part, ld);
-                    else if (lvl2) dma16<false>(rs_dst, vo, so_part, ld);
-                    else dma16<false>(rs_src, vo, so_part, ld);
-                }
+                if (lvl2) dma16<true>(rs_dst, vo, so_part, ld);
+                else dma16<false>(rs_src, vo, so_part, ld);
             }
         }
     };
@@ -353,106 +286,39 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
 #pragma unroll
     for (int i = 0; i < kSlots; i++) sl[i] = 0;
 
-#ifdef TEC_DMA_CENSUS
-    // timing builds only: (cu key, start, end) per workgroup into a.scratch
-    uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-#endif
-    if constexpr (TEC_DMA_LOADER) {
-        if (wv == (uint32_t)G) {
-            // the loader: every plane's DMA, two planes ahead of the compute; the barriers
-            // mirror the compute waves' B2 / B1 (the ring slot of plane z is free after B1 of z)
-            if constexpr (TEC_DMA_LPRIO) __builtin_amdgcn_s_setprio(TEC_DMA_LPRIO);
-            if constexpr (TEC_DMA_DIRECT) {
-                // three slots: plane z + 3 goes into plane z's slot after B1 of z; before B1 of
-                // z, plane z + 1 must have landed (plane z + 2's 23 pieces may still be in flight)
-                issue_dma(0, 0);
-                issue_dma(1, kSlotBytes);
-                issue_dma(2, 2 * kSlotBytes);
-                asm volatile("s_waitcnt vmcnt(46)\n\ts_barrier" ::: "memory");  // plane 0 landed
-                uint32_t sl3 = 0;  // z % 3
-                for (uint32_t z = 0; z < (uint32_t)(kQ * kQ); z++) {
-                    if (z + 2u < (uint32_t)(kQ * kQ))
-                        asm volatile("s_waitcnt vmcnt(23)" ::: "memory");
-                    else
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    lds_barrier();  // B1
-                    if (z + 3u < (uint32_t)(kQ * kQ)) issue_dma(z + 3u, sl3 * kSlotBytes);
-                    sl3 = sl3 == 2u ? 0u : sl3 + 1u;
-                }
-                return;
-            }
-            issue_dma(0, 0);
-            issue_dma(1, kSlotBytes);
-            asm volatile("s_waitcnt vmcnt(23)\n\ts_barrier" ::: "memory");  // plane 0 landed
-            for (uint32_t z = 0; z < (uint32_t)(kQ * kQ); z++) {
-                lds_barrier();                                  // B2
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // plane z + 1 landed
-                lds_barrier();                                  // B1
-                if (z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, (z & 1u) * kSlotBytes);
-            }
-            return;
-        }
-        asm volatile("s_barrier" ::: "memory");
-    } else {
+    if (wv == (uint32_t)G) {
+        // the loader: every plane's DMA, two planes ahead of the compute; the barriers mirror
+        // the compute waves' B2 / B1 (the ring slot of plane z is free after B1 of z)
         issue_dma(0, 0);
         issue_dma(1, kSlotBytes);
-        asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");  // plane 0 landed (3 <= pieces of plane 1)
+        asm volatile("s_waitcnt vmcnt(23)\n\ts_barrier" ::: "memory");  // plane 0 landed
+        for (uint32_t z = 0; z < (uint32_t)(kQ * kQ); z++) {
+            lds_barrier();                                  // B2
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // plane z + 1 landed
+            lds_barrier();                                  // B1
+            if (z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, (z & 1u) * kSlotBytes);
+        }
+        return;
     }
+    asm volatile("s_barrier" ::: "memory");
 
     uint8_t *const stg = lds8 + kStageBase + colw;
-    uint32_t prev_n = 0;  // ORDER 2: rows this wave stored last step (2 store instructions each)
-    // DIRECT: a lane stores its word of each output row itself; the word straddling the row end
-    // (sc = 2 mod 4) is two bytes, stored with a 16-bit store by its wave only
-    const uint32_t vo_w = (threadIdx.x < RB * 4u && colw + 4u <= sc) ? colw : kDrop;
-    const uint32_t tw = sc >> 2;  // the straddling word (when sc % 4 == 2)
-    const bool tail_wave = (sc & 2u) && wv == tw / 64u;
-    const uint32_t vo_t = (threadIdx.x == tw) ? colw : kDrop;
-    uint32_t ring = 0;  // DIRECT: z % 3
     for (uint32_t z0 = 0; z0 < (uint32_t)kQ; z0++) {
         const bool lvl2 = z0 >= (uint32_t)K;
         const uint32_t type = lvl2 ? z0 - (K - 1) : 0u;
         for (uint32_t s = 0; s < (uint32_t)kQ; s++) {
             const uint32_t z = z0 * kQ + s;
-            const uint32_t slot = TEC_DMA_DIRECT ? ring * kSlotBytes : (z & 1u) * kSlotBytes;
+            const uint32_t slot = (z & 1u) * kSlotBytes;
             const uint8_t *img = lds8 + slot + colw;
-            // an output row of this step: staging row `r` (the flush table's numbering) or, DIRECT,
-            // the lane's word straight to its chunk at its plane
-            auto out = [&](int r, uint32_t v) {
-                if constexpr (!TEC_DMA_DIRECT) {
-                    st32(stg + r * RW, v);
-                } else {
-                    uint32_t node, plane;
-                    if (r >= kRowB) node = kQ + s, plane = z0 * kQ + (uint32_t)(r - kRowB);        // C(10+s, (z0, j))
-                    else if (r >= kRowC1) node = kQ + (uint32_t)(r - kRowC1), plane = z;         // C(10+j, (z0, s))
-                    else if (r >= kRowX) node = z0, plane = (uint32_t)(K + r - kRowX) * kQ + s;  // C(z0, (7+i, s))
-                    else node = (uint32_t)(K + r - kRowC0), plane = z;                            // node 7+r
-                    if (TEC_DMA_STORE_MASK && !((store_mask >> node) & 1u)) return;  // a chunk the caller does not keep
-                    const uint32_t so = slice_off(node) + plane * sc;
-                    if (!(TEC_DMA_ABLATE & 1)) {
-                        __builtin_amdgcn_raw_buffer_store_b32(v, rb_dst, (int)vo_w, (int)so, TEC_DMA_ST_AUX);
-                        if (tail_wave) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rb_dst, (int)vo_t, (int)so, TEC_DMA_ST_AUX);
-                    }
-                }
-            };
+            // an output row of this step: staging row `r` (the flush table's numbering)
+            auto out = [&](int r, uint32_t v) { st32(stg + r * RW, v); };
             // ---- compute ----
-            if constexpr (TEC_DMA_PRIO) __builtin_amdgcn_s_setprio(TEC_DMA_PRIO);
             uint32_t own[K], part[kQ];
 #pragma unroll
             for (int x = 0; x < K; x++) own[x] = lds32(img + x * RW);
             if (z == ez) {  // end-row substitution, also patched into the image the flush copies
                 own[ex] = fixw;
-                if constexpr (!TEC_DMA_DIRECT) st32(lds8 + slot + ex * RW + colw, fixw);
-            }
-            if constexpr (TEC_DMA_DIRECT) {  // systematic rows: the input words as they are
-                if (!(TEC_DMA_ABLATE & 1)) {
-#pragma unroll
-                    for (int x = 0; x < K; x++) {
-                        if (TEC_DMA_STORE_MASK && !((store_mask >> x) & 1u)) continue;
-                        const uint32_t so = slice_off((uint32_t)x) + z * sc;
-                        __builtin_amdgcn_raw_buffer_store_b32(own[x], rb_dst, (int)vo_w, (int)so, TEC_DMA_ST_AUX);
-                        if (tail_wave) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)own[x], rb_dst, (int)vo_t, (int)so, TEC_DMA_ST_AUX);
-                    }
-                }
+                st32(lds8 + slot + ex * RW + colw, fixw);
             }
             uint32_t acc[20 - K];
             if (!lvl2) {
@@ -463,8 +329,7 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
                 uint32_t u[K];
 #pragma unroll
                 for (int x = 0; x < K; x++) u[x] = (uint32_t)x == z0 ? own[x] : pft3(own[x], part[x]);
-                if constexpr (TEC_DMA_SLP && !(TEC_DMA_ABLATE & 4)) enc::mds7_slp<true>(u, acc);
-                else enc::mds_rows<K, true, (TEC_DMA_ABLATE & 4) != 0>(u, acc);
+                enc::mds7_slp<true>(u, acc);
 #pragma unroll
                 for (int r = 0; r < 3; r++)
                     out(kRowC0 + r, acc[r] ^ mulc(kPft.t_p[1], part[K + r]));
@@ -474,8 +339,7 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
                 uint32_t u[K];
 #pragma unroll
                 for (int x = 0; x < K; x++) u[x] = pft3(own[x], part[x]);
-                if constexpr (TEC_DMA_SLP && !(TEC_DMA_ABLATE & 4)) enc::mds7_slp<false>(u, acc);
-                else enc::mds_rows<K, false, (TEC_DMA_ABLATE & 4) != 0>(u, acc);
+                enc::mds7_slp<false>(u, acc);
                 const uint32_t i0 = z0 - K;
 #pragma unroll
                 for (int r = 0; r < 3; r++) {
@@ -486,7 +350,7 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
                         const uint32_t tt = xt(us ^ up);
                         // C(z0, (7+r, s)): a row only for r < i0 (staged unconditionally, flushed
                         // only then)
-                        if (!TEC_DMA_DIRECT || (uint32_t)r < i0) out(kRowX + r, us ^ tt);
+                        out(kRowX + r, us ^ tt);
                         out(kRowC0 + r, (uint32_t)r < i0 ? up ^ tt : up);  // C / U(7+r, (z0, s))
                     } else {
                         out(kRowC0 + r, acc[r]);
@@ -505,17 +369,7 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
                 case 8: col1<8>(acc + 3, sl, out); break;
                 default: col1<9>(acc + 3, sl, out); break;
             }
-            if constexpr (TEC_DMA_PRIO) __builtin_amdgcn_s_setprio(TEC_DMA_KPRIO);
-            if constexpr (TEC_DMA_DIRECT) {
-                // B1 only: every wave is done reading this slot; stores older than ~2 steps have
-                // landed (<= kDirectLag in flight), so the slice rows a later DMA reads back
-                // (level-2 partners, >= 8 steps later) are there
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDirectLag) : "memory");
-                lds_barrier();
-                ring = ring == 2u ? 0u : ring + 1u;
-                continue;
-            }
-            if constexpr (!(TEC_DMA_ABLATE & 16)) lds_barrier();  // B2: the plane's rows are staged
+            lds_barrier();  // B2: the plane's rows are staged
             // ---- flush: this wave's share, read now, stored after B1 ----
             const FlushTab::W &F = kFlush.w[type][s][wv];
             const uint32_t n = F.n;
@@ -531,69 +385,36 @@ __global__ void __launch_bounds__(kWaves * 64, TEC_DMA_WPE) enc_dma_kernel(EncAr
                     d1[q] = *reinterpret_cast<const u32x4 *>(row + lo1);
                     const uint32_t node = (it >> 8) & 0xffu, tz0 = (it >> 16) & 0xffu, ts = it >> 24;
                     dst[q] = slice_off(node) + ((tz0 == 0xffu ? z0 : tz0) * kQ + (ts == 0xffu ? s : ts)) * sc;
-                    if (TEC_DMA_STORE_MASK && !((store_mask >> node) & 1u)) dst[q] = kDrop;  // a chunk the caller does not keep
+                    if (!((store_mask >> node) & 1u)) dst[q] = kDrop;  // a chunk the caller does not keep
                 }
             }
-            // B1: the next plane's DMA has landed (this wave's pieces are older than its last
-            // step's >= 2 stores) and every wave is done reading this slot and the staging rows
-            if constexpr (TEC_DMA_LOADER) {
-                // no loads to wait for: only bound the stores in flight (see kStoreLag)
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kStoreLag) : "memory");
-            } else if constexpr (!(TEC_DMA_ABLATE & 8)) {
-                if constexpr (TEC_DMA_ORDER == 2) {
-                    // outstanding, oldest first: the next plane's DMA pieces, then the previous
-                    // step's 2 x prev_n stores -- wait for the DMA only
-                    switch (prev_n) {
-                        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-                        case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-                        case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-                        case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-                        case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-                        default: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-                    }
-                } else if (TEC_DMA_ORDER || z == 0) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                } else {
-                    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-                }
-            }
+            // B1: the next plane's DMA has landed and every wave is done reading this slot and the
+            // staging rows; the compute waves issue no loads, so they only bound their stores in
+            // flight (see kStoreLag)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kStoreLag) : "memory");
             lds_barrier();
-            if (!TEC_DMA_LOADER && TEC_DMA_ORDER != 1 && z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, slot);
-            prev_n = (TEC_DMA_ABLATE & 1) ? 0u : n;
 #pragma unroll
             for (int q = 0; q < kCap; q++) {
-                if ((uint32_t)q < n && !(TEC_DMA_ABLATE & 1)) {
-                    __builtin_amdgcn_raw_buffer_store_b128(d0[q], rb_dst, (int)vo0, (int)dst[q], TEC_DMA_ST_AUX);
-                    __builtin_amdgcn_raw_buffer_store_b128(d1[q], rb_dst, (int)vo1, (int)dst[q], TEC_DMA_ST_AUX);
+                if ((uint32_t)q < n) {
+                    __builtin_amdgcn_raw_buffer_store_b128(d0[q], rb_dst, (int)vo0, (int)dst[q], kStAux);
+                    __builtin_amdgcn_raw_buffer_store_b128(d1[q], rb_dst, (int)vo1, (int)dst[q], kStAux);
                 }
             }
-            if (!TEC_DMA_LOADER && TEC_DMA_ORDER == 1 && z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, slot);
         }
     }
     // the last plane's left-over row (its staging row is untouched since the last compute)
-    if (!TEC_DMA_DIRECT && wv == 0) {
+    if (wv == 0) {
         const uint32_t it = kFlush.extra, src = it & 0xffu;
         const uint8_t *row = lds8 + kStageBase + src * RW;
         const u32x4 e0 = *reinterpret_cast<const u32x4 *>(row + lo0);
         const u32x4 e1 = *reinterpret_cast<const u32x4 *>(row + lo1);
         const uint32_t node = (it >> 8) & 0xffu, tz0 = (it >> 16) & 0xffu, ts = it >> 24;
-        const uint32_t d = (!TEC_DMA_STORE_MASK || ((store_mask >> node) & 1u))
+        const uint32_t d = ((store_mask >> node) & 1u)
                                ? slice_off(node) + ((tz0 == 0xffu ? kQ - 1u : tz0) * kQ + (ts == 0xffu ? kQ - 1u : ts)) * sc
                                : kDrop;
-        if (!(TEC_DMA_ABLATE & 1)) {
-            __builtin_amdgcn_raw_buffer_store_b128(e0, rb_dst, (int)vo0, (int)d, TEC_DMA_ST_AUX);
-            __builtin_amdgcn_raw_buffer_store_b128(e1, rb_dst, (int)vo1, (int)d, TEC_DMA_ST_AUX);
-        }
+        __builtin_amdgcn_raw_buffer_store_b128(e0, rb_dst, (int)vo0, (int)d, kStAux);
+        __builtin_amdgcn_raw_buffer_store_b128(e1, rb_dst, (int)vo1, (int)d, kStAux);
     }
-#ifdef TEC_DMA_CENSUS
-    if (threadIdx.x == 0) {
-        const uint32_t hw = __builtin_amdgcn_s_getreg(63492), xcc = __builtin_amdgcn_s_getreg(63508);
-        uint64_t *rec = reinterpret_cast<uint64_t *>(a.scratch) + 3 * blockIdx.x;
-        rec[0] = ((uint64_t)(xcc & 0xf) << 32) | (hw & 0xff00u);
-        rec[1] = t_start;
-        rec[2] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
 }
 
 }  // namespace dma
@@ -605,12 +426,12 @@ hipError_t launch_encode_dma(bool masked, const EncArgs &a, hipStream_t s) {
     if (!encode_dma_supported((int)a.n, 7, a.sc) || a.njobs > 0x7fffffffu) return hipErrorInvalidValue;
     const void *fn = masked ? reinterpret_cast<const void *>(dma::enc_dma_kernel<true>)
                             : reinterpret_cast<const void *>(dma::enc_dma_kernel<false>);
-    hipError_t e = ensure_dyn_lds(fn, dma::kLdsLaunch);
+    hipError_t e = ensure_dyn_lds(fn, dma::kLdsBytes);
     if (e != hipSuccess) return e;
     if (masked)
-        hipLaunchKernelGGL(dma::enc_dma_kernel<true>, dim3(a.njobs), dim3(dma::kWaves * 64), dma::kLdsLaunch, s, a);
+        hipLaunchKernelGGL(dma::enc_dma_kernel<true>, dim3(a.njobs), dim3(dma::kWaves * 64), dma::kLdsBytes, s, a);
     else
-        hipLaunchKernelGGL(dma::enc_dma_kernel<false>, dim3(a.njobs), dim3(dma::kWaves * 64), dma::kLdsLaunch, s, a);
+        hipLaunchKernelGGL(dma::enc_dma_kernel<false>, dim3(a.njobs), dim3(dma::kWaves * 64), dma::kLdsBytes, s, a);
     return hipGetLastError();
 }
 
