@@ -381,16 +381,12 @@ static hipError_t launch_dec_g(const DecArgs &a, uint64_t blocks, hipStream_t s)
     return hipGetLastError();
 }
 
-template <int NK>
+// waves per workgroup g <= kMaxG: only 1..kMaxG are built (unreachable bodies)
+template <int NK, int G = dstage::kMaxG>
 static hipError_t launch_dec_k(const DecArgs &a, uint32_t g, uint64_t blocks, hipStream_t s) {
-    switch (g) {
-        case 1: return launch_dec_g<NK, 1>(a, blocks, s);
-        case 2: return launch_dec_g<NK, 2>(a, blocks, s);
-        case 3: return launch_dec_g<NK, 3>(a, blocks, s);
-        case 4: return launch_dec_g<NK, 4>(a, blocks, s);
-        case 5: return launch_dec_g<NK, 5>(a, blocks, s);
-        default: return launch_dec_g<NK, 6>(a, blocks, s);
-    }
+    if constexpr (G > 1)
+        if (g < (uint32_t)G) return launch_dec_k<NK, G - 1>(a, g, blocks, s);
+    return launch_dec_g<NK, G>(a, blocks, s);
 }
 
 hipError_t launch_decode_stage(DecArgs a, hipStream_t s) {

@@ -2648,6 +2648,33 @@ int te_recover_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t 
         chunk[i] = g.chunk_size;
         for (int w = 0; w < 6; w++) meta_w[i * 6 + w] = get_u64(h_meta + i * TE_META_SIZE + 8 * w);
     }
+    // A mixed batch goes in two parts: the objects the fused path takes (a plane-program profile,
+    // sub-chunks of >= 8 bytes, 31-bit slice offsets: decode_enqueue's staged_group) and the rest,
+    // so one small object does not send the whole batch to the windowed decode + re-encode
+    // (ADVICE r03).  Offsets are absolute, so each part is the same call on a subset.
+    {
+        const bool planes = h.q == kRepQ && h.t == 2 && h.nu == 0;
+        std::vector<size_t> part[2];
+        for (size_t i = 0; i < nobj; i++) {
+            const uint64_t sc = chunk[i] / (uint64_t)h.alpha;
+            const bool fz = planes && (items[i].ns == 0 || sc >= 8) && (uint64_t)n * objs[i].slice_len < 0x7fffffffull &&
+                            chunk[i] * (uint64_t)h.k < 0x7fffffffull;
+            part[fz ? 0 : 1].push_back(i);
+        }
+        if (!part[0].empty() && !part[1].empty()) {
+            for (const auto &pv : part) {
+                std::vector<te_recover_object> o;
+                std::vector<uint8_t> m;
+                for (size_t i : pv) {
+                    o.push_back(objs[i]);
+                    m.insert(m.end(), h_meta + i * TE_META_SIZE, h_meta + (i + 1) * TE_META_SIZE);
+                }
+                const int r = te_recover_batch_device(c, cfg, d_slices, o.data(), m.data(), o.size(), d_out, stream);
+                if (r) return r;
+            }
+            return TE_OK;
+        }
+    }
     {
         // Fused: one staged decode whose program outputs only the lost node's chunk of every stripe,
         // straight into the lost slice -- 7 slices read, 1 written, no decoded object and no

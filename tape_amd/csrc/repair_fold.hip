@@ -341,6 +341,13 @@ static hipError_t launch_fold_g(const RepArgs &a, uint64_t blocks, hipStream_t s
     return hipGetLastError();
 }
 
+template <int G>
+static hipError_t fold_dispatch(uint32_t g, const RepArgs &a, uint64_t blocks, hipStream_t s) {
+    if constexpr (G > 1)
+        if (g < (uint32_t)G) return fold_dispatch<G - 1>(g, a, blocks, s);
+    return launch_fold_g<G>(a, blocks, s);
+}
+
 hipError_t launch_repair_fold(RepArgs a, hipStream_t s) {
     if (a.njobs == 0) return hipSuccess;
     if (a.sc < 8) return hipErrorInvalidValue;
@@ -349,14 +356,8 @@ hipError_t launch_repair_fold(RepArgs a, hipStream_t s) {
     a.wgs_per_stripe = (groups + g - 1) / g;
     const uint64_t blocks = (uint64_t)a.njobs * a.wgs_per_stripe;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    switch (g) {  // waves per workgroup: sub-chunks below 6 x 256 bytes use fewer
-        case 1: return launch_fold_g<1>(a, blocks, s);
-        case 2: return launch_fold_g<2>(a, blocks, s);
-        case 3: return launch_fold_g<3>(a, blocks, s);
-        case 4: return launch_fold_g<4>(a, blocks, s);
-        case 5: return launch_fold_g<5>(a, blocks, s);
-        default: return launch_fold_g<6>(a, blocks, s);
-    }
+    // waves per workgroup (g <= kMaxG; small sub-chunks use fewer): only 1..kMaxG are built
+    return fold_dispatch<rfold::kMaxG>(g, a, blocks, s);
 }
 
 }  // namespace tec

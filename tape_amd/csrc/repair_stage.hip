@@ -204,6 +204,13 @@ static hipError_t launch_rep_stage_g(const RepArgs &a, uint64_t blocks, hipStrea
     return hipGetLastError();
 }
 
+template <int G>
+static hipError_t rep_stage_dispatch(uint32_t g, const RepArgs &a, uint64_t blocks, hipStream_t s) {
+    if constexpr (G > 1)
+        if (g < (uint32_t)G) return rep_stage_dispatch<G - 1>(g, a, blocks, s);
+    return launch_rep_stage_g<G>(a, blocks, s);
+}
+
 hipError_t launch_repair_stage(RepArgs a, hipStream_t s) {
     if (a.njobs == 0) return hipSuccess;
     const uint32_t groups = (a.words_per_stripe + 63) / 64;
@@ -211,14 +218,7 @@ hipError_t launch_repair_stage(RepArgs a, hipStream_t s) {
     a.wgs_per_stripe = (groups + g - 1) / g;
     const uint64_t blocks = (uint64_t)a.njobs * a.wgs_per_stripe;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    switch (g) {
-        case 1: return launch_rep_stage_g<1>(a, blocks, s);
-        case 2: return launch_rep_stage_g<2>(a, blocks, s);
-        case 3: return launch_rep_stage_g<3>(a, blocks, s);
-        case 4: return launch_rep_stage_g<4>(a, blocks, s);
-        case 5: return launch_rep_stage_g<5>(a, blocks, s);
-        default: return launch_rep_stage_g<6>(a, blocks, s);
-    }
+    return rep_stage_dispatch<rstage::kMaxG>(g, a, blocks, s);  // only 1..kMaxG waves are built
 }
 
 }  // namespace tec

@@ -179,3 +179,40 @@ def test_recover_batch_4mib_random_peers(oracle):
     got = d_rec.cpu().numpy()
     for i in range(nobj):
         assert np.array_equal(got[i * g.slice_len:(i + 1) * g.slice_len], exp[i]), i
+
+
+@pytest.mark.parametrize("small_only", [False, True])
+def test_recover_mixed_batch_split(oracle, small_only):
+    """A batch mixing 4 MiB objects (fused decode: 7 slices in, the lost one out) with tiny objects
+    whose sub-chunks are below the staged kernel's 8 bytes (windowed decode + re-encode) recovers
+    every object: the batch is split by path (one small object used to send the whole
+    batch to the windowed path).  small_only: the windowed path on its own."""
+    import torch
+    from tape_amd import batch
+    sizes = [1000, 3000] if small_only else [4 * MiB, 1000, 4 * MiB + 8, 3000, 2 * MiB]
+    s = T.Slicer.clay_default()
+    geo = [s.geometry(L) for L in sizes]
+    datas = [oracle.splitmix64_bytes(0x51 + i, L).tobytes() for i, L in enumerate(sizes)]
+    enc = [T.Slicer.clay_default().encode(d) for d in datas]
+    for e, d in zip(enc, datas):
+        assert e == oracle.slicer_encode(oracle.OracleClay(20, 7, 16), d)
+    host, offs, a = bytearray(), [], 0
+    for e in enc:
+        offs.append(len(host))
+        host += b"".join(e)
+    d_sl = torch.frombuffer(bytes(host), dtype=torch.uint8).cuda()
+    rnd = random.Random(len(sizes))
+    objs, metas, exp, out_off = [], b"", [], 0
+    for i, (g, e) in enumerate(zip(geo, enc)):
+        lost = rnd.randrange(N)
+        avail = rnd.sample([j for j in range(N) if j != lost], 7)
+        objs.append((offs[i], g.slice_len, sum(1 << j for j in avail), lost, out_off))
+        metas += e[0][-48:]
+        exp.append((out_off, e[lost]))
+        out_off += g.slice_len
+    d_rec = torch.zeros(out_off, dtype=torch.uint8, device="cuda")
+    batch.recover_batch(s, d_sl, objs, metas, d_rec)
+    torch.cuda.synchronize()
+    got = d_rec.cpu().numpy().tobytes()
+    for i, (o, sl) in enumerate(exp):
+        assert got[o:o + len(sl)] == sl, i
