@@ -108,6 +108,34 @@ def traffic_key(mode: str, pattern: str = "worst") -> str:
     return "decode:random" if mode == "decode" and pattern == "random" else mode
 
 
+def gpu_env(torch, dev) -> dict:
+    """The box the line was measured on (two box types answer the same binary 0.41 vs
+    0.47): device name, CUs, and from sysfs (best effort, read-only) the current GPU / memory clock
+    levels and the compute / memory partition modes of this GPU's PCI function."""
+    out = {}
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        out.update(name=p.name, arch=p.gcnArchName, cus=p.multi_processor_count,
+                   pci=f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}")
+        base = f"/sys/bus/pci/devices/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        for key, fn in (("sclk", "pp_dpm_sclk"), ("mclk", "pp_dpm_mclk"), ("fclk", "pp_dpm_fclk")):
+            try:
+                lines = open(os.path.join(base, fn)).read().split("\n")
+                cur = [l for l in lines if l.strip().endswith("*")]
+                out[key] = (cur[0] if cur else " | ".join(l for l in lines if l)).strip()
+            except OSError:
+                pass
+        for key, fn in (("compute_partition", "current_compute_partition"),
+                        ("memory_partition", "current_memory_partition")):
+            try:
+                out[key] = open(os.path.join(base, fn)).read().strip()
+            except OSError:
+                pass
+    except Exception as e:  # never fail a bench line on this
+        out["error"] = str(e)[:80]
+    return out
+
+
 def rank_objects(rank: int, nobj: int) -> tuple[int, int]:
     """Contiguous global object range [first, first + nobj) of this rank (weak scaling)."""
     return rank * nobj, rank * nobj + nobj
@@ -386,6 +414,7 @@ def main():
                          "alg_bytes_per_launch": unit_bytes * nobj if unit_bytes else None,
                          "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
             "cpu_baseline": cpu,
+            "gpu": gpu_env(torch, dev),
             "copy_inclusive": copy_inc,
             "copy_inclusive_encode_commit": copy_commit,
             "commit_GiBps_vs_objects": commit_sweep,

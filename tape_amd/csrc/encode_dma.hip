@@ -1,11 +1,10 @@
 // encode_dma.hip -- Clay(20,7,16) layered encode of 1 MB stripes (sub-chunk 1,281..1,440 bytes),
 // row by row per plane.  Replaces ClayCoder::encode -> clay_codes::ClayCode::encode
 // (lib/slicer/src/clay.rs:99-104) in Slicer::encode's stripe loop (slicer.rs:268-286), fused
-// with distribute_chunks' rotation (slicer.rs:60-71).  Since r04 the production kernel for the
-// common case is encode_r10.hip (row-of-planes pieces); this one serves the stripes that kernel
-// leaves: objects at 2-mod-4 offsets, a data end inside a dword (MASKED), chunk filters
-// (te_recover_batch_device's re-encode), other sub-chunk sizes.  Same algebra and plane order as
-// encode_stage.hip; what differs is how bytes move:
+// with distribute_chunks' rotation (slicer.rs:60-71): the production hot path.  Same algebra and
+// plane order as encode_stage.hip; what differs is how bytes
+// move (a row-of-planes variant that stores 14,300-byte pieces measured slower as a skeleton at
+// one workgroup per CU, profiles/r04_enc_skeleton4.txt):
 //   * inputs arrive by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per wave-instruction, from
 //     2-aligned addresses -- scripts/ldsdma_probe.hip) into a two-slot ring of plane images,
 //     one plane ahead, issued by a dedicated loader wave: 23 wave-instructions per plane;

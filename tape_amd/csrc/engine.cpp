@@ -34,17 +34,12 @@ namespace {
 constexpr size_t kStripeSizes[3] = {100000, 1000000, 10000000};  // adaptive.rs:15-19
 
 thread_local char g_last_error[256] = "";
-// TEC_ENCODE_KERNEL=stage / dma selects an earlier 1 MB-stripe encode kernel (measurement only)
+// TEC_ENCODE_KERNEL=stage selects the previous 1 MB-stripe encode kernel (measurement only)
 const bool g_no_dma_encode = [] {
     const char *e = tec_knob("TEC_ENCODE_KERNEL");
     return e && strcmp(e, "stage") == 0;
 }();
-// the row-piece kernel (encode_r10.hip): on with TEC_ENCODE_KERNEL=r10 until it has passed the
-// GPU parity suite
-const bool g_no_r10_encode = [] {
-    const char *e = tec_knob("TEC_ENCODE_KERNEL");
-    return !(e && strcmp(e, "r10") == 0);
-}();
+
 // TEC_REPAIR_KERNEL=stage keeps the folded repair kernel off (measurement / cross-check only)
 const bool g_no_fold_repair = [] {
     const char *e = tec_knob("TEC_REPAIR_KERNEL");
@@ -648,13 +643,10 @@ struct GeomKey {
     bool odd;     // stripe data at an odd address: the fast kernels load 4 bytes at 2-aligned
                   // addresses only (an odd-address dword near the data end reads short through
                   // the range check), so such stripes take the generic byte-exact kernel
-    bool r10 = false;  // the row-piece kernel's case (encode_r10.hip): 1 MB stripes, input and
-                       // slices 4-aligned, whole dwords of data, every chunk written
     bool operator<(const GeomKey &o) const {
         if (cs != o.cs) return cs < o.cs;
         if (slice_len != o.slice_len) return slice_len < o.slice_len;
         if (odd != o.odd) return odd < o.odd;
-        if (r10 != o.r10) return r10 < o.r10;
         return masked < o.masked;
     }
 };
@@ -711,10 +703,7 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
             j.dst_skew = (uint32_t)(st * cs);
             const bool masked = ((reinterpret_cast<uintptr_t>(j.src) & 3u) + j.src_len) % 4 != 0;
             const bool odd = (reinterpret_cast<uintptr_t>(j.src) & 1u) != 0;
-            const bool r10 = !masked && ((reinterpret_cast<uintptr_t>(j.src) | reinterpret_cast<uintptr_t>(j.dst)) & 3u) == 0 &&
-                             store == ~0u && encode_r10_supported(n, h.k, (uint32_t)(cs / (size_t)h.alpha)) &&
-                             !g_no_r10_encode;
-            groups[GeomKey{cs, slice_len, masked, odd, r10}].push_back(j);
+            groups[GeomKey{cs, slice_len, masked, odd}].push_back(j);
         }
         if (!raw && !keep) {
             MetaJob m{};
@@ -810,16 +799,7 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
         const uint32_t wps = (sc + 3) / 4;   // words incl. a 2-column tail when sc % 4 == 2
         const uint32_t full = sc / 4;        // full 4-column words
         // fast kernel addresses an object's slices with 31-bit buffer offsets
-        if (L.key.r10 && fast_path(L)) {  // the 1 MB-stripe row-piece kernel (encode_r10.hip)
-            EncArgs a{};
-            a.jobs = A.at<EncJob>(L.off);
-            a.njobs = (uint32_t)L.count;
-            a.cs = cs;
-            a.sc = sc;
-            a.slice_len = (uint32_t)L.key.slice_len;
-            a.n = (uint32_t)n;
-            TE_HIP(launch_encode_r10(a, s));
-        } else if (dma_path(L)) {  // the 1 MB-stripe kernel (encode_dma.hip)
+        if (dma_path(L)) {  // the 1 MB-stripe kernel (encode_dma.hip)
             EncArgs a{};
             a.jobs = A.at<EncJob>(L.off);
             a.njobs = (uint32_t)L.count;

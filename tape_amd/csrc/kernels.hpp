@@ -245,8 +245,6 @@ hipError_t launch_commit(const CommitArgs &a, hipStream_t s);
 
 hipError_t launch_encode_rows(int k, bool masked, const EncArgs &a, hipStream_t s);
 // encode_dma.hip: Clay(20,7,16), 1,280 < sub-chunk <= 1,440 bytes (the 1 MB stripes), no scratch
-bool encode_r10_supported(int n, int k, uint32_t sc);
-hipError_t launch_encode_r10(const EncArgs &a, hipStream_t s);
 bool encode_dma_supported(int n, int k, uint32_t sc);
 hipError_t launch_encode_dma(bool masked, const EncArgs &a, hipStream_t s);
 hipError_t launch_meta(const MetaJob *jobs, uint32_t njobs, uint32_t n, hipStream_t s);
