@@ -125,6 +125,10 @@ def gpu_env(torch, dev) -> dict:
                 out[key] = (cur[0] if cur else " | ".join(l for l in lines if l)).strip()
             except OSError:
                 pass
+        try:
+            out["host_cpu"] = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+        except (OSError, StopIteration):
+            pass
         for key, fn in (("compute_partition", "current_compute_partition"),
                         ("memory_partition", "current_memory_partition")):
             try:
@@ -161,6 +165,8 @@ def main():
     ap.add_argument("--chunk-bytes", type=int, default=64 * MiB,
                     help="--mode stream: MAX_TRACK_SIZE, the SDK's stream chunk (sdk/src/stream/manifest.rs:22)")
     ap.add_argument("--stream-chunks", type=int, default=64, help="--mode stream: chunks per rank per pass")
+    ap.add_argument("--hash-threads", type=int, default=0,
+                    help="--mode stream: host hashing pool size (0 = the library's default, min(16, affinity CPUs))")
     ap.add_argument("--in-flight", type=int, default=4,
                     help="--mode stream: MAX_ENCODE_WORKERS, chunk encodes in flight (sdk/src/stream/write.rs:54-57)")
     ap.add_argument("--segments", type=int, default=16,
@@ -533,6 +539,8 @@ def stream_bench(args, torch, dist, world, rank, dev):
     import tape_amd as T
     from tape_amd import batch, merkle
     CB, nch, depth, H = args.chunk_bytes, args.stream_chunks, args.in_flight, T.SLICE_TREE_HEIGHT
+    if args.hash_threads:
+        batch.set_host_hash_threads(args.hash_threads)
     s = T.Slicer.clay_default()
     g = s.geometry(CB)
     per = N * g.slice_len
@@ -608,7 +616,7 @@ def stream_bench(args, torch, dist, world, rank, dev):
             ok = ok and pv[j * H * 32:(j + 1) * H * 32] == b"".join(merkle.create_proof_from_leaf_hashes(leaves, j, H))
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline_stream(args, ring_auto, CB, R)
+        cpu = cpu_baseline_stream(args, ring_auto, CB, R, first)
     if rank == 0:
         print(json.dumps({
             "metric": "copy-inclusive stream write GiB/s (64 MiB chunks, encode_with_proofs per chunk, <= 4 in flight), "
@@ -623,7 +631,8 @@ def stream_bench(args, torch, dist, world, rank, dev):
                        "host_hash_threads": batch.host_hash_threads(),
                        "host_sha_extensions": bool(T.lib.te_host_sha_extensions()),
                        "parallelism": f"chunks partitioned over {world} GPU(s)"},
-            "legs": legs, "roofline": None, "cpu_baseline": cpu, "outputs_verified": bool(ok)}), flush=True)
+            "legs": legs, "roofline": None, "cpu_baseline": cpu, "gpu": gpu_env(torch, dev),
+            "outputs_verified": bool(ok)}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -727,7 +736,7 @@ def cpu_baseline_percall(src, out, sl, L, stripe):
             "cores": 1, "kind": "port", "encode_equal": bool((exp.reshape(-1) == out).all())}
 
 
-def cpu_baseline_stream(args, r, CB, R):
+def cpu_baseline_stream(args, r, CB, R, first=0):
     """The reference's stream encode on host cores: per chunk the oracle's Slicer::encode (C
     restatement, AVX2 region multiply) + hashlib SHA-256 leaves + merkle root and proofs (the
     oracle's), one chunk per thread: on 16 threads (the GPU's host share) and on MAX_ENCODE_WORKERS
@@ -737,9 +746,12 @@ def cpu_baseline_stream(args, r, CB, R):
     from oracle import oracle as O
     from oracle import merkle_oracle as MO
     clay = O.OracleClay(20, 7, 16)
+    nch = args.stream_chunks
+    # the chunk each ring slot held last (its metadata suffix names that chunk's index)
+    chunk_of = [first + k + R * ((nch - 1 - k) // R) for k in range(R)]
 
     def one(k):
-        sl = O.slicer_encode_np(clay, r["in"][k].numpy())
+        sl = O.slicer_encode_np(clay, r["in"][k].numpy(), chunk_index=chunk_of[k])
         leaves = []
         for j in range(N):
             h = hashlib.sha256(b"LEAF")

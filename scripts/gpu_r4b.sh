@@ -1,0 +1,11 @@
+#!/bin/bash
+# round-4 GPU call: whole GPU suite (verbose, per-test limit), smoke, default bench line, stream-shape line
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r4b
+mkdir -p $O
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
+tail -5 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && cat $O/smoke.log &&
+timeout -k 10 600 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err && cat $O/bench_default.json &&
+timeout -k 10 400 python -u bench.py --mode stream > $O/bench_stream.json 2> $O/bench_stream.err && cat $O/bench_stream.json
