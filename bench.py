@@ -629,6 +629,7 @@ def stream_bench(args, torch, dist, world, rank, dev):
                                    f"{depth} in flight (te_stream_writer)", "chunk_bytes": CB,
                        "slice_len": g.slice_len, "in_flight": depth, "profile": "clay(20,7,16)",
                        "host_hash_threads": batch.host_hash_threads(),
+                       "host_hash_GBps_per_thread": round(T.lib.te_host_hash_rate() / 1e9, 3),
                        "host_sha_extensions": bool(T.lib.te_host_sha_extensions()),
                        "parallelism": f"chunks partitioned over {world} GPU(s)"},
             "legs": legs, "roofline": None, "cpu_baseline": cpu, "gpu": gpu_env(torch, dev),
@@ -899,17 +900,21 @@ def copy_inclusive_commit(args, torch, dist, world, slicer, batch, d_in, d_out, 
                 sw.wait(t - 4)
         sw.wait(t)
 
-    for wobj in (64, 128, 256):
-        if wobj > m:
-            continue
-        run_stream(wobj)  # warm-up (buffers)
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.copy_steps):
-            run_stream(wobj)
-        el = max_over_ranks(torch, dist, world, time.perf_counter() - t0, dev)
-        stream[f"window_{wobj}_objects_GiBps"] = round(m * world * args.copy_steps * L / el / 2**30, 3)
+    # the library's per-window choice of who hashes (auto), and each side forced
+    for hashing in ("auto", "device", "host"):
+        sw.set_hashing(hashing)
+        for wobj in (64, 128, 256):
+            if wobj > m:
+                continue
+            run_stream(wobj)  # warm-up (buffers)
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.copy_steps):
+                run_stream(wobj)
+            el = max_over_ranks(torch, dist, world, time.perf_counter() - t0, dev)
+            key = f"window_{wobj}_objects_GiBps" + ("" if hashing == "auto" else f"_{hashing}_hashing")
+            stream[key] = round(m * world * args.copy_steps * L / el / 2**30, 3)
     sw.close()
     ok2 = bool(torch.equal(h_out[:per], d_out[:per].cpu()))
     return {"value": best, "unit": "GiB/s", "objects_per_gpu": m, "steps": args.copy_steps, "pinned": True,

@@ -316,6 +316,7 @@ int te_stream_writer_set_hashing(te_stream_writer *w, int mode);
 int te_set_host_hash_threads(int threads);
 int te_host_hash_threads(void);
 int te_host_sha_extensions(void);     /* 1 if the host SHA-256 uses the CPU's SHA extensions */
+double te_host_hash_rate(void);       /* one pool thread's leaf-hash rate, bytes/s (measured at start) */
 
 /* Page-locked host memory for the host <-> device entry points (te_encode_*_host, te_stream_submit,
  * the per-call te_slicer_* / te_clay_* calls): copies from it run at full PCIe rate and need no

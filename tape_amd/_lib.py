@@ -157,6 +157,7 @@ def _load() -> C.CDLL:
         "te_set_host_hash_threads": (i, [i]),
         "te_host_hash_threads": (i, []),
         "te_host_sha_extensions": (i, []),
+        "te_host_hash_rate": (C.c_double, []),
         "te_host_alloc": (i, [sz, C.POINTER(vp)]),
         "te_host_free": (None, [vp]),
         "te_host_register": (i, [vp, sz]),

@@ -2008,7 +2008,8 @@ static int group_close(CommitPipe &P, OpenGroup &G, uint32_t n, uint32_t height,
 
 // Who hashes a group (te_set_commit_hashing / te_stream_writer_set_hashing, TE_HASH_*).  A leaf
 // launch hashes one slice per lane at ~24 MB/s per lane (715,048 B in ~29.5 ms)
-// whatever the number of slices up to ~64k of them; the host pool hashes ~1.5 GB/s per thread.
+// whatever the number of slices up to ~64k of them; the host pool hashes at its measured
+// per-thread rate (SHA extensions: 1-2 GB/s) times its threads.
 // The device wins for many short slices (a batch of 4 MiB objects), the host for few long ones
 // (the SDK's 64 MiB chunks, ~9.7 MB slices, <= 4 in flight: ~0.4 s per leaf launch).
 std::atomic<int> g_commit_hashing{TE_HASH_AUTO};
@@ -2016,7 +2017,8 @@ bool host_hash_wins(int mode, uint64_t streams, uint64_t max_slice, uint64_t sli
     if (mode == TE_HASH_HOST) return true;
     if (mode == TE_HASH_DEVICE) return false;
     const double dev_s = (double)max_slice / 24e6 * std::max(1.0, (double)streams / 65536.0);
-    const double host_s = (double)slice_bytes / (1.5e9 * hh::Pool::get().threads());
+    const hh::Pool &pool = hh::Pool::get();
+    const double host_s = (double)slice_bytes / (pool.thread_rate() * pool.threads());
     return host_s < dev_s;
 }
 
@@ -2487,6 +2489,8 @@ int te_set_host_hash_threads(int threads) {
 int te_host_hash_threads(void) { return hh::Pool::get().threads(); }
 
 int te_host_sha_extensions(void) { return hh::have_sha_ext() ? 1 : 0; }
+
+double te_host_hash_rate(void) { return hh::Pool::get().thread_rate(); }
 
 int te_host_alloc(size_t bytes, void **out) {
     if (!out) return TE_ERR_INVALID_ARG;

@@ -4,6 +4,9 @@
 #include <sched.h>
 #include <string.h>
 
+#include <algorithm>
+#include <chrono>
+
 #include "sha256.hpp"
 
 #if defined(__x86_64__)
@@ -142,7 +145,17 @@ Pool &Pool::get() {
     return *p;
 }
 
-Pool::Pool() { start(default_threads()); }
+Pool::Pool() {
+    // calibrate the per-thread rate the device / host choice uses (host_hash_wins): hash 4 MiB
+    std::vector<uint8_t> buf((size_t)4 << 20, 0x5a);
+    uint8_t out[32];
+    hash_leaf(buf.data(), 4096, out);  // warm up
+    const auto t0 = std::chrono::steady_clock::now();
+    hash_leaf(buf.data(), buf.size(), out);
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (dt > 0) rate_ = std::min(8e9, std::max(1e8, (double)buf.size() / dt));
+    start(default_threads());
+}
 Pool::~Pool() { stop(); }
 
 void Pool::start(int n) {

@@ -62,6 +62,8 @@ class Pool {
     // default: min(16, CPUs this process may run on) -- 16 is a GPU's host share on the pool
     // this runs on; te_set_host_hash_threads changes it (idle pool only)
     int threads() const { return nthreads_; }
+    // one thread's SHA-256 rate (bytes/s), measured once on this host (a 4 MiB hash at startup)
+    double thread_rate() const { return rate_; }
     int set_threads(int n);
     // run `tasks` once `ev` (on `device`, may be null) has completed; the pool destroys `ev`
     void submit_after(hipEvent_t ev, int device, std::vector<std::function<void()>> tasks);
@@ -85,6 +87,7 @@ class Pool {
     bool quit_ = false;
     int nthreads_ = 0;
     int busy_ = 0;
+    double rate_ = 1.5e9;
 };
 
 int default_threads();
