@@ -698,7 +698,7 @@ def percall_bench(args, torch, dist, world, rank, dev):
                 for _ in range(reps):
                     fn()
                 ms = (time.perf_counter() - t) / reps * 1e3
-                row[name] = {"ms_per_call": round(ms, 3), "GiBps": round(L / ms / 1e3 / 2**30 * 1e3, 3)}
+                row[name] = {"ms_per_call": round(ms, 3), "object_GiBps": round(L / (ms / 1e3) / 2**30, 3)}
             ok = ok and np.array_equal(dec, src) and np.array_equal(rep, out[:sl])
             res[f"{L >> 20}MiB_{kind}"] = row
         if rank == 0 and args.cpu_sample > 0:

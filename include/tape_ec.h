@@ -112,8 +112,13 @@ int te_clay_set_decode_jit(te_clay *c, int mode, uint64_t min_stripes);
 /* Pattern kernels ready / compiling / failed on the handle, after waiting up to `timeout_ms` for
  * compiles in flight to finish. */
 int te_clay_decode_jit_status(te_clay *c, uint32_t timeout_ms, uint32_t *ready, uint32_t *pending, uint32_t *failed);
+/* Most distinct stripe patterns the handle's device-resident decode store holds (default and
+ * maximum 16,384, ~26 KB of device memory and as much host memory each; the store grows by
+ * doubling from 256 as patterns arrive).  A call with more distinct patterns than this uploads
+ * them with the call. */
+int te_clay_set_decode_store_cap(te_clay *c, uint32_t max_patterns);
 /* The handle's device-resident decode pattern store (diagnostics): slots allocated (it grows by
- * doubling from 256 to 8192, ~26 KB of device memory each) and filled, how often a full store was
+ * doubling from 256 up to the cap) and filled, how often a full store was
  * emptied, how often it grew, and how many calls had more distinct stripe patterns than it holds
  * (those upload their patterns with the call instead). */
 int te_clay_decode_store_stats(te_clay *c, uint32_t *capacity, uint32_t *used, uint64_t *clears, uint64_t *grows,

@@ -200,6 +200,11 @@ impl ClayCoder {
         if s != 0 { fatal(s) }
         (r, p, f)
     }
+    /// Most distinct stripe patterns the device decode store keeps (default 16,384).
+    pub fn set_decode_store_cap(&mut self, max_patterns: u32) {
+        let r = unsafe { ffi::te_clay_set_decode_store_cap(self.raw.as_ptr(), max_patterns) };
+        if r != 0 { fatal(r) }
+    }
     /// The device decode-pattern store: (capacity, filled, clears, grows, over-capacity calls).
     pub fn decode_store_stats(&self) -> (u32, u32, u64, u64, u64) {
         let (mut cap, mut used, mut cl, mut gr, mut ar) = (0u32, 0u32, 0u64, 0u64, 0u64);

@@ -108,6 +108,7 @@ def _load() -> C.CDLL:
         "te_clay_device": (i, [vp]),
         "te_clay_set_decode_jit": (i, [vp, i, u64]),
         "te_clay_decode_jit_status": (i, [vp, u32, u32p, u32p, u32p]),
+        "te_clay_set_decode_store_cap": (i, [vp, u32]),
         "te_clay_decode_store_stats": (i, [vp, u32p, u32p, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)]),
         "te_version": (C.c_char_p, []),
         "te_kernel_timing": (C.c_int, [C.c_int]),

@@ -280,12 +280,15 @@ struct te_clay {
     // call cost more host time than the kernel takes.  Slots are handed out in order; a full store
     // is emptied after its last reader (`used`) has finished.
     // The store grows by doubling from kMin slots (each slot ~26 KB of device memory: 102 steps
-    // of DecStepP plus its GpePattern and header; kCap slots = ~215 MB) once its last reader is
-    // done.  New slots are filled with stream-ordered copies from the call's descriptor upload
+    // of DecStepP plus its GpePattern and header; kCap slots = ~430 MB; te_clay_set_decode_store_cap
+    // lowers the cap) once its last reader is done.  New slots are filled with stream-ordered copies from the call's descriptor upload
     // (decode_enqueue), never with a host-blocking copy; a call on another stream waits for the
     // last fill (`written`) before reading.
     struct DecStore {
-        static constexpr uint32_t kCap = 8192, kMin = 256;
+        // 16,384: a batch of 2,048 x 4 MiB reads with random survivor sets has ~10,000 distinct
+        // stripe patterns; at 8,192 every such call overflowed to per-call uploads and recompiles
+        static constexpr uint32_t kCap = 16384, kMin = 256;
+        uint32_t max_cap = kCap;
         static constexpr uint32_t kSteps = kRepQ * kRepQ + 2;  // 100 planes + 2 blank steps
         DevBuf pats, hdrs, steps, soff;
         uint32_t cap = 0;
@@ -511,6 +514,22 @@ int te_clay_set_decode_jit(te_clay *c, int mode, uint64_t min_stripes) {
     c->jit_mode = mode;
     c->jit_min = min_stripes;
     if (c->jit) dec_jit_set(c->jit, mode, min_stripes);
+    return TE_OK;
+}
+
+int te_clay_set_decode_store_cap(te_clay *c, uint32_t max_patterns) {
+    if (!c || max_patterns < 1 || max_patterns > te_clay::DecStore::kCap) return TE_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    te_clay::DecStore &S = c->dstore;
+    if (S.cap > max_patterns) {  // shrink: the store is re-allocated at the next decode
+        if (S.used_pending) (void)hipEventSynchronize(S.used);
+        S.used_pending = false;
+        for (DevBuf *b : {&S.pats, &S.hdrs, &S.steps, &S.soff}) b->release();
+        S.cap = 0;
+        S.slot.clear();
+        S.n = 0;
+    }
+    S.max_cap = max_patterns;
     return TE_OK;
 }
 
@@ -963,9 +982,10 @@ struct StoreFill {
 bool dec_store_slots(te_clay *c, const std::vector<const te_clay::DecCache *> &cached, const std::vector<uint64_t> &keys,
                      std::vector<uint32_t> &slot_of, StoreFill &U, int &rc) {
     te_clay::DecStore &S = c->dstore;
-    constexpr uint32_t kCap = te_clay::DecStore::kCap, kSteps = te_clay::DecStore::kSteps;
+    constexpr uint32_t kSteps = te_clay::DecStore::kSteps;
     rc = TE_OK;
-    if (keys.size() > kCap) {
+    const uint32_t cap_max = S.max_cap;
+    if (keys.size() > cap_max) {
         S.arena_calls++;
         return false;
     }
@@ -978,11 +998,11 @@ bool dec_store_slots(te_clay *c, const std::vector<const te_clay::DecCache *> &c
     if (S.n + fresh > S.cap) {
         // grow (doubling, up to kCap) when the call's patterns do not fit, else empty the full
         // store; either way the old contents go once their last reader is done
-        const uint32_t need = (uint32_t)std::min<size_t>(kCap, std::max<size_t>(keys.size(), (size_t)S.n + fresh));
-        if (S.cap < kCap && need > S.cap) {
-            uint32_t cap = std::max(te_clay::DecStore::kMin, S.cap);
+        const uint32_t need = (uint32_t)std::min<size_t>(cap_max, std::max<size_t>(keys.size(), (size_t)S.n + fresh));
+        if (S.cap < cap_max && need > S.cap) {
+            uint32_t cap = std::min(te_clay::DecStore::kMin, cap_max);
             while (cap < need) cap *= 2;
-            cap = std::min(cap, kCap);
+            cap = std::min(cap, cap_max);
             // the buffers are freed: every launch that read them must be done (rare: <= 6 times)
             if (S.used_pending && (rc = hip_status(hipEventSynchronize(S.used)))) return false;
             S.used_pending = false;
@@ -1030,9 +1050,9 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     const ClayHost &h = c->h;
     const int n = h.n;
     const int rotated = (cfg && !raw) ? cfg->rotated : 0;
-    // <= ~215 MB of host memory (26 KB per pattern; 77,520 masks exist for k = 7, x 20 outputs
-    // for node recover)
-    if (c->dec_cache.size() > te_clay::DecStore::kCap) c->dec_cache.clear();
+    // compiled programs kept on the host: <= ~430 MB (26 KB per pattern, as many as the device
+    // store's cap; 77,520 masks exist for k = 7, x 20 outputs for node recover)
+    if (c->dec_cache.size() > std::max<size_t>(c->dstore.max_cap, nitems)) c->dec_cache.clear();
     {
         std::vector<std::pair<uint64_t, int>> keys;
         std::unordered_map<uint64_t, char> seen;

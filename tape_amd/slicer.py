@@ -283,6 +283,10 @@ class ClayCoder:
         if r:
             raise _engine_error(r)
 
+    def set_decode_store_cap(self, max_patterns: int) -> None:
+        """te_clay_set_decode_store_cap: most distinct stripe patterns kept on the device."""
+        _check(lib.te_clay_set_decode_store_cap(self.handle, max_patterns), "decode")
+
     def decode_store_stats(self) -> dict:
         """te_clay_decode_store_stats: the device pattern store's capacity, filled slots, clears,
         grows and over-capacity (arena) calls."""

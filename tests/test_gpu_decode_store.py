@@ -2,8 +2,9 @@
 
 Slicer::decode from any k slices (lib/slicer/src/slicer.rs:298-364; the SDK's downloader takes
 whichever k arrive, sdk/src/transfer/downloader.rs:79-109), so a batch of reads has one erasure
-pattern per stripe.  The engine keeps compiled patterns in a device-resident store of at most
-8,192 slots that grows by doubling (te_clay::DecStore):
+pattern per stripe.  The engine keeps compiled patterns in a device-resident store that grows by
+doubling up to its cap (16,384 by default; these tests set 8,192 with te_clay_set_decode_store_cap
+to keep them small):
   * one call with more distinct stripe patterns than the store holds uploads its patterns with
     the call (the arena path);
   * calls whose union overflows the store empty it once its last reader is done (the clear path).
@@ -58,6 +59,7 @@ def test_decode_store_arena_path():
     import torch
     s = T.Slicer.clay_default()
     s.coder.set_decode_jit("off")
+    s.coder.set_decode_store_cap(8192)
     nobj = 9000
     d_in, d_out, g, per, meta = _encoded(torch, s, nobj, 11)
     masks = _masks(random.Random(5), nobj)
@@ -78,6 +80,7 @@ def test_decode_store_clear_path():
     import torch
     s = T.Slicer.clay_default()
     s.coder.set_decode_jit("off")
+    s.coder.set_decode_store_cap(8192)
     nobj = 5000
     d_in, d_out, g, per, meta = _encoded(torch, s, nobj, 12)
     m1 = _masks(random.Random(7), nobj)
@@ -114,3 +117,21 @@ def test_decode_store_two_streams():
     batch.decode_batch(s, d_out, objs, meta * nobj, o2, s2)  # same patterns, read on s2
     torch.cuda.synchronize()
     assert torch.equal(o1, d_in) and torch.equal(o2, d_in)
+
+
+def test_decode_store_default_cap_holds_2048_random_objects():
+    """The default cap holds the ~10,000 stripe patterns of 2,048 random-survivor reads in place:
+    a second call over the same patterns compiles and uploads nothing (no arena call, no clear)."""
+    import torch
+    s = T.Slicer.clay_default()
+    s.coder.set_decode_jit("off")
+    nobj = 10_000  # one stripe each: ~2,048 x 4 MiB objects' worth of distinct patterns
+    d_in, d_out, g, per, meta = _encoded(torch, s, nobj, 14)
+    masks = _masks(random.Random(10), nobj)
+    a = _decode(torch, s, d_out, g, per, meta, masks)
+    st1 = s.coder.decode_store_stats()
+    b = _decode(torch, s, d_out, g, per, meta, masks)
+    st2 = s.coder.decode_store_stats()
+    assert torch.equal(a, d_in) and torch.equal(b, d_in)
+    assert st1["arena_calls"] == 0 and st1["capacity"] == 16384 and st1["used"] == nobj, st1
+    assert st2 == st1, (st1, st2)
