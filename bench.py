@@ -562,15 +562,26 @@ def stream_bench(args, torch, dist, world, rank, dev):
 
     descs = [batch.encode_descs([(0, CB, 0, first + c)]) for c in range(nch)]
 
+    lat = []  # per chunk: submit -> its wait returned (the SDK's FuturesOrdered hand-off)
+
     def run(sw, r, chunks):
         inflight = collections.deque()
+        t_sub = {}
+        del lat[:]
         for c in range(chunks):
             k = c % R
             if len(inflight) >= depth:
-                sw.wait(inflight.popleft())
-            inflight.append(sw.submit(r["in"][k], descs[c], r["out"][k], r["leaf"][k], r["root"][k], r["proof"][k]))
-        if inflight:
-            sw.wait(inflight[-1])
+                t = inflight.popleft()
+                sw.wait(t)
+                lat.append(time.perf_counter() - t_sub.pop(t))
+            t_sub_c = time.perf_counter()
+            t = sw.submit(r["in"][k], descs[c], r["out"][k], r["leaf"][k], r["root"][k], r["proof"][k])
+            t_sub[t] = t_sub_c
+            inflight.append(t)
+        while inflight:
+            t = inflight.popleft()
+            sw.wait(t)
+            lat.append(time.perf_counter() - t_sub.pop(t))
 
     def leg(hashing, pinned):
         r = ring(pinned)
@@ -588,7 +599,10 @@ def stream_bench(args, torch, dist, world, rank, dev):
     for name, hashing, pinned in (("auto_pinned", "auto", True), ("host_hash_pinned", "host", True),
                                   ("device_hash_pinned", "device", True), ("auto_pageable", "auto", False)):
         v, el, r = leg(hashing, pinned)
-        legs[name] = {"GiBps": round(v, 3), "ms_per_chunk": round(el / nch * 1e3, 2)}
+        ls = sorted(lat)
+        legs[name] = {"GiBps": round(v, 3), "ms_per_chunk": round(el / nch * 1e3, 2),
+                      "chunk_latency_ms_p50_p90": [round(ls[len(ls) // 2] * 1e3, 2), round(ls[(9 * len(ls)) // 10] * 1e3, 2)]
+                      if ls else None}
         if name == "auto_pinned":
             ring_auto, el_auto = r, el
         else:
