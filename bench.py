@@ -628,6 +628,17 @@ def stream_bench(args, torch, dist, world, rank, dev):
         pv = ring_auto["proof"][k].numpy().tobytes()
         for j in range(N):
             ok = ok and pv[j * H * 32:(j + 1) * H * 32] == b"".join(merkle.create_proof_from_leaf_hashes(leaves, j, H))
+    # one thread's leaf-hash rate over one chunk's 20 slices at 1-4 interleaved lanes (te_hash_leaves;
+    # the pool runs te_host_hash_lanes of them per task)
+    lane_rate = []
+    if rank == 0:
+        import ctypes as C
+        sl = ring_auto["out"][0]
+        hout = (C.c_uint8 * (32 * N))()
+        for L in range(1, 5):
+            t = time.perf_counter()
+            T.lib.te_hash_leaves(C.cast(sl.data_ptr(), C.POINTER(C.c_uint8)), g.slice_len, N, L, hout)
+            lane_rate.append(round(N * g.slice_len / (time.perf_counter() - t) / 1e9, 3))
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         cpu = cpu_baseline_stream(args, ring_auto, CB, R, first)
@@ -644,6 +655,8 @@ def stream_bench(args, torch, dist, world, rank, dev):
                        "slice_len": g.slice_len, "in_flight": depth, "profile": "clay(20,7,16)",
                        "host_hash_threads": batch.host_hash_threads(),
                        "host_hash_GBps_per_thread": round(T.lib.te_host_hash_rate() / 1e9, 3),
+                       "host_hash_lanes": T.lib.te_host_hash_lanes(),
+                       "host_hash_GBps_one_thread_at_lanes_1_to_4": lane_rate,
                        "host_sha_extensions": bool(T.lib.te_host_sha_extensions()),
                        "parallelism": f"chunks partitioned over {world} GPU(s)"},
             "legs": legs, "roofline": None, "cpu_baseline": cpu, "gpu": gpu_env(torch, dev),

@@ -322,6 +322,10 @@ int te_set_host_hash_threads(int threads);
 int te_host_hash_threads(void);
 int te_host_sha_extensions(void);     /* 1 if the host SHA-256 uses the CPU's SHA extensions */
 double te_host_hash_rate(void);       /* one pool thread's leaf-hash rate, bytes/s (measured at start) */
+/* Slices one pool task hashes together, interleaved round by round (1..4): the lane count whose
+ * measured per-thread rate is best on this host (a lone SHA-256 chain leaves the CPU's SHA unit
+ * idle between dependent rounds). */
+int te_host_hash_lanes(void);
 
 /* Page-locked host memory for the host <-> device entry points (te_encode_*_host, te_stream_submit,
  * the per-call te_slicer_* / te_clay_* calls): copies from it run at full PCIe rate and need no
@@ -383,6 +387,10 @@ int te_recover_batch_device(te_clay *c, const te_slicer_cfg *cfg, const uint8_t 
 
 /* hash_leaf (tree.rs:53-56): SHA-256("LEAF" || data).  Host. */
 int te_hash_leaf(const uint8_t *data, size_t len, uint8_t out[TE_HASH_SIZE]);
+/* hash_leaf of `count` messages of `len` bytes each at data + i*len (an object's slices, as
+ * encoder.rs:226-229 hashes them one by one) into out + i*32, `lanes` (1..4; 0 = te_host_hash_lanes)
+ * of them interleaved on the calling thread.  Host. */
+int te_hash_leaves(const uint8_t *data, size_t len, size_t count, uint32_t lanes, uint8_t *out);
 /* hash_pair (tree.rs:58-62): SHA-256("LEFT" || left || "RIGHT" || right).  Host. */
 int te_hash_pair(const uint8_t left[TE_HASH_SIZE], const uint8_t right[TE_HASH_SIZE], uint8_t out[TE_HASH_SIZE]);
 /* empty_subtree_root / EMPTY_ROOTS[height] (tree.rs:15-48, 64-68), height < 32.  Host. */

@@ -159,6 +159,7 @@ def _load() -> C.CDLL:
         "te_host_hash_threads": (i, []),
         "te_host_sha_extensions": (i, []),
         "te_host_hash_rate": (C.c_double, []),
+        "te_host_hash_lanes": (i, []),
         "te_host_alloc": (i, [sz, C.POINTER(vp)]),
         "te_host_free": (None, [vp]),
         "te_host_register": (i, [vp, sz]),
@@ -169,6 +170,7 @@ def _load() -> C.CDLL:
         "te_recover_batch_device": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_recover_object), u8p, sz,
                                         vp, vp]),
         "te_hash_leaf": (i, [u8p, sz, u8p]),
+        "te_hash_leaves": (i, [u8p, sz, sz, u32, u8p]),
         "te_hash_pair": (i, [u8p, u8p, u8p]),
         "te_empty_subtree_root": (i, [u32, u8p]),
         "te_merkle_root_from_leaf_hashes": (i, [u8p, sz, u32, u8p]),

@@ -1926,8 +1926,9 @@ static int host_tree(const uint8_t *leaf, uint32_t n, uint32_t height, uint8_t *
 }
 
 // Host-hashed close (host_hash.hpp):the group's slices are hashed from the host output buffers
-// once their D2H copies have landed -- one pool task per slice, the object's root and proofs by
-// whichever of its slice tasks finishes last.  The group buffer is free as soon as the copies are
+// once their D2H copies have landed -- one pool task per te_host_hash_lanes slices of an object
+// (interleaved, hh::hash_leaves), the object's root and proofs by whichever of its tasks finishes
+// last.  The group buffer is free as soon as the copies are
 // done.  Returns the job the window tickets wait for.
 static int group_close_host(CommitPipe &P, OpenGroup &G, uint32_t n, uint32_t height, int device,
                             std::shared_ptr<hh::Job> &job) {
@@ -1947,6 +1948,7 @@ static int group_close_host(CommitPipe &P, OpenGroup &G, uint32_t n, uint32_t he
     }
     job = std::make_shared<hh::Job>();
     std::vector<std::function<void()>> tasks;
+    const uint32_t lanes = (uint32_t)hh::Pool::get().lanes();
     for (const GroupSeg &sg : G.segs) {
         for (size_t q = 0; q < sg.cnt; q++) {
             const uint8_t *slices = sg.h_out + sg.h_off[q];
@@ -1955,11 +1957,19 @@ static int group_close_host(CommitPipe &P, OpenGroup &G, uint32_t n, uint32_t he
             uint8_t *root = sg.co.root + (sg.obj0 + q) * TE_HASH_SIZE;
             uint8_t *proof = sg.co.proof ? sg.co.proof + (sg.obj0 + q) * (uint64_t)n * height * TE_HASH_SIZE : nullptr;
             auto left = std::make_shared<std::atomic<uint32_t>>(n);
-            for (uint32_t i = 0; i < n; i++)
+            // one task per `lanes` slices of the object (hash_leaves interleaves them)
+            for (uint32_t i0 = 0; i0 < n; i0 += lanes)
                 tasks.push_back([=, j = job.get()] {
-                    hh::hash_leaf(slices + (uint64_t)i * slen, slen, leaf + (uint64_t)i * TE_HASH_SIZE);
+                    const uint32_t L = std::min(lanes, n - i0);
+                    const uint8_t *src[hh::kMaxLanes];
+                    uint8_t *dst[hh::kMaxLanes];
+                    for (uint32_t l = 0; l < L; l++) {
+                        src[l] = slices + (uint64_t)(i0 + l) * slen;
+                        dst[l] = leaf + (uint64_t)(i0 + l) * TE_HASH_SIZE;
+                    }
+                    hh::hash_leaves((int)L, src, slen, dst);
                     int rc = TE_OK;
-                    if (left->fetch_sub(1) == 1) rc = host_tree(leaf, n, height, root, proof);
+                    if (left->fetch_sub(L) == L) rc = host_tree(leaf, n, height, root, proof);
                     j->done(rc);
                 });
         }
@@ -2511,6 +2521,8 @@ int te_host_hash_threads(void) { return hh::Pool::get().threads(); }
 int te_host_sha_extensions(void) { return hh::have_sha_ext() ? 1 : 0; }
 
 double te_host_hash_rate(void) { return hh::Pool::get().thread_rate(); }
+
+int te_host_hash_lanes(void) { return hh::Pool::get().lanes(); }
 
 int te_host_alloc(size_t bytes, void **out) {
     if (!out) return TE_ERR_INVALID_ARG;
@@ -3192,6 +3204,22 @@ int te_clay_repair(te_clay *c, uint32_t lost, const uint32_t *helpers, const uin
 int te_hash_leaf(const uint8_t *data, size_t len, uint8_t out[TE_HASH_SIZE]) {
     if ((!data && len) || !out) return TE_ERR_INVALID_ARG;
     hh::hash_leaf(data, len, out);
+    return TE_OK;
+}
+
+int te_hash_leaves(const uint8_t *data, size_t len, size_t count, uint32_t lanes, uint8_t *out) {
+    if ((!data && len && count) || (!out && count) || lanes > (uint32_t)hh::kMaxLanes) return TE_ERR_INVALID_ARG;
+    if (lanes == 0) lanes = (uint32_t)hh::Pool::get().lanes();
+    const uint8_t *src[hh::kMaxLanes];
+    uint8_t *dst[hh::kMaxLanes];
+    for (size_t i0 = 0; i0 < count; i0 += lanes) {
+        const int L = (int)std::min<size_t>(lanes, count - i0);
+        for (int l = 0; l < L; l++) {
+            src[l] = data + (i0 + l) * len;
+            dst[l] = out + (i0 + l) * TE_HASH_SIZE;
+        }
+        hh::hash_leaves(L, src, len, dst);
+    }
     return TE_OK;
 }
 

@@ -30,6 +30,9 @@ namespace hh {
 // SHA-256("LEAF" || data) (lib/crypto/src/merkle/tree.rs:53-56): x86 SHA extensions when the CPU
 // has them, the portable compression (sha256.hpp) otherwise.
 void hash_leaf(const uint8_t *data, size_t len, uint8_t out[32]);
+// The same for L <= kMaxLanes messages of one length, interleaved round by round on one thread.
+constexpr int kMaxLanes = 4;
+void hash_leaves(int L, const uint8_t *const *data, size_t len, uint8_t *const *out);
 bool have_sha_ext();
 
 // A set of tasks whose completion a ticket waits for.
@@ -62,8 +65,11 @@ class Pool {
     // default: min(16, CPUs this process may run on) -- 16 is a GPU's host share on the pool
     // this runs on; te_set_host_hash_threads changes it (idle pool only)
     int threads() const { return nthreads_; }
-    // one thread's SHA-256 rate (bytes/s), measured once on this host (a 4 MiB hash at startup)
+    // one thread's SHA-256 rate (bytes/s) at lanes() interleaved messages, measured once on this
+    // host at startup; lane_rate(L) the rate measured at L lanes
     double thread_rate() const { return rate_; }
+    int lanes() const { return lanes_; }
+    double lane_rate(int L) const { return L >= 1 && L <= kMaxLanes ? lane_rate_[L - 1] : 0.0; }
     int set_threads(int n);
     // run `tasks` once `ev` (on `device`, may be null) has completed; the pool destroys `ev`
     void submit_after(hipEvent_t ev, int device, std::vector<std::function<void()>> tasks);
@@ -88,6 +94,8 @@ class Pool {
     int nthreads_ = 0;
     int busy_ = 0;
     double rate_ = 1.5e9;
+    int lanes_ = 1;
+    double lane_rate_[kMaxLanes] = {};
 };
 
 int default_threads();

@@ -59,6 +59,20 @@ def hash_leaf(data: bytes) -> bytes:
     return bytes(out)
 
 
+def hash_leaves(data: bytes, count: int, lanes: int = 0) -> list:
+    """hash_leaf of `count` equal-length pieces of `data` (an object's slices), `lanes` of them
+    interleaved on this thread (0 = the host's best, te_host_hash_lanes)."""
+    b = bytes(data)
+    if count <= 0 or len(b) % count:
+        raise ValueError("data must split into count equal pieces")
+    ln = len(b) // count
+    buf = (C.c_uint8 * max(1, len(b))).from_buffer_copy(b or b"\0")
+    out = (C.c_uint8 * (HASH_SIZE * count))()
+    _check(lib.te_hash_leaves(buf, ln, count, lanes, out))
+    o = bytes(out)
+    return [o[i * HASH_SIZE:(i + 1) * HASH_SIZE] for i in range(count)]
+
+
 def hash_pair(left: bytes, right: bytes) -> bytes:
     out = _out()
     _check(lib.te_hash_pair(_hashes([left]), _hashes([right]), out))

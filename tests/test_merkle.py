@@ -48,6 +48,27 @@ def test_lib_hashes_match_oracle(M):
     assert M.hash_pair(a, b) != M.hash_pair(b, a)
 
 
+@pytest.mark.parametrize("lanes", [0, 1, 2, 3, 4])
+def test_lib_interleaved_leaves_match_oracle(M, lanes):
+    # te_hash_leaves: 1-4 messages interleaved round by round (the host pool's tasks); every count
+    # leaves a short last group
+    rnd = random.Random(11 + lanes)
+    for ln in (0, 3, 59, 60, 61, 123, 124, 125, 4096, 70_001):
+        for count in (1, 2, 3, 4, 5, 7, 20):
+            d = os.urandom(ln * count) if ln > 1000 else bytes(rnd.getrandbits(8) for _ in range(ln * count))
+            got = M.hash_leaves(d, count, lanes) if ln else M.hash_leaves(b"", count, lanes)
+            want = [O.hash_leaf(d[i * ln:(i + 1) * ln]) for i in range(count)]
+            assert got == want, (ln, count)
+    with pytest.raises(Exception):
+        M.hash_leaves(b"abc", 2)
+
+
+def test_host_hash_lanes(M):
+    from tape_amd import _lib
+    assert 1 <= _lib.lib.te_host_hash_lanes() <= 4
+    assert _lib.lib.te_hash_leaves(None, 0, 1, 5, None) == _lib.TE_ERR_INVALID_ARG
+
+
 def test_two_leaves(M):  # tree.rs:503-517
     l1, l2 = M.hash_leaf(b"hello"), M.hash_leaf(b"world")
     assert M.root_from_leaf_hashes([l1, l2], 1) == M.hash_pair(l1, l2)
