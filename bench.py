@@ -562,12 +562,12 @@ def stream_bench(args, torch, dist, world, rank, dev):
 
     descs = [batch.encode_descs([(0, CB, 0, first + c)]) for c in range(nch)]
 
-    lat = []  # per chunk: submit -> its wait returned (the SDK's FuturesOrdered hand-off)
+    lat, sub = [], []  # per chunk: submit -> its wait returned (the SDK's FuturesOrdered hand-off); the submit call
 
     def run(sw, r, chunks):
         inflight = collections.deque()
         t_sub = {}
-        del lat[:]
+        del lat[:], sub[:]
         for c in range(chunks):
             k = c % R
             if len(inflight) >= depth:
@@ -576,6 +576,7 @@ def stream_bench(args, torch, dist, world, rank, dev):
                 lat.append(time.perf_counter() - t_sub.pop(t))
             t_sub_c = time.perf_counter()
             t = sw.submit(r["in"][k], descs[c], r["out"][k], r["leaf"][k], r["root"][k], r["proof"][k])
+            sub.append(time.perf_counter() - t_sub_c)
             t_sub[t] = t_sub_c
             inflight.append(t)
         while inflight:
@@ -602,7 +603,8 @@ def stream_bench(args, torch, dist, world, rank, dev):
         ls = sorted(lat)
         legs[name] = {"GiBps": round(v, 3), "ms_per_chunk": round(el / nch * 1e3, 2),
                       "chunk_latency_ms_p50_p90": [round(ls[len(ls) // 2] * 1e3, 2), round(ls[(9 * len(ls)) // 10] * 1e3, 2)]
-                      if ls else None}
+                      if ls else None,
+                      "submit_call_ms_mean_max": [round(sum(sub) / len(sub) * 1e3, 3), round(max(sub) * 1e3, 3)] if sub else None}
         if name == "auto_pinned":
             ring_auto, el_auto = r, el
         else:
@@ -630,7 +632,7 @@ def stream_bench(args, torch, dist, world, rank, dev):
             ok = ok and pv[j * H * 32:(j + 1) * H * 32] == b"".join(merkle.create_proof_from_leaf_hashes(leaves, j, H))
     # one thread's leaf-hash rate over one chunk's 20 slices at 1-4 interleaved lanes (te_hash_leaves;
     # the pool runs te_host_hash_lanes of them per task)
-    lane_rate = []
+    lane_rate, pool_rate = [], None
     if rank == 0:
         import ctypes as C
         sl = ring_auto["out"][0]
@@ -639,6 +641,25 @@ def stream_bench(args, torch, dist, world, rank, dev):
             t = time.perf_counter()
             T.lib.te_hash_leaves(C.cast(sl.data_ptr(), C.POINTER(C.c_uint8)), g.slice_len, N, L, hout)
             lane_rate.append(round(N * g.slice_len / (time.perf_counter() - t) / 1e9, 3))
+        # the pool's share of host cores hashing at once: one thread per te_host_hash_lanes slices
+        # of the ring's chunks (ctypes drops the GIL), as the pool's tasks do
+        import threading
+        lanes = T.lib.te_host_hash_lanes()
+        jobs = [(k, i0) for k in range(R) for i0 in range(0, N, lanes)]
+        nthr = batch.host_hash_threads()
+        outs = [(C.c_uint8 * (32 * N))() for _ in range(nthr)]
+
+        def worker(w):
+            for k, i0 in jobs[w::nthr]:
+                base = ring_auto["out"][k].data_ptr() + i0 * g.slice_len
+                T.lib.te_hash_leaves(C.cast(base, C.POINTER(C.c_uint8)), g.slice_len, min(lanes, N - i0), lanes, outs[w])
+        ths = [threading.Thread(target=worker, args=(w,)) for w in range(nthr)]
+        t = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        pool_rate = round(R * N * g.slice_len / (time.perf_counter() - t) / 1e9, 2)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         cpu = cpu_baseline_stream(args, ring_auto, CB, R, first)
@@ -657,6 +678,7 @@ def stream_bench(args, torch, dist, world, rank, dev):
                        "host_hash_GBps_per_thread": round(T.lib.te_host_hash_rate() / 1e9, 3),
                        "host_hash_lanes": T.lib.te_host_hash_lanes(),
                        "host_hash_GBps_one_thread_at_lanes_1_to_4": lane_rate,
+                       "host_hash_GBps_all_threads": pool_rate,
                        "host_sha_extensions": bool(T.lib.te_host_sha_extensions()),
                        "parallelism": f"chunks partitioned over {world} GPU(s)"},
             "legs": legs, "roofline": None, "cpu_baseline": cpu, "gpu": gpu_env(torch, dev),

@@ -1782,6 +1782,73 @@ static void commit_plan(const CommitBatch &B, uint64_t group_bytes, uint64_t cop
     }
 }
 
+// One object's slices copied out in row pieces (host-hashed groups, pinned host output): piece p
+// is bytes [beg[p], beg[p+1]) of every slice, landed once ev[p] has completed.  The host hashing
+// tasks follow the pieces as they land instead of waiting for the whole window's D2H.
+struct PieceEvents {
+    int device = 0;
+    std::vector<hipEvent_t> ev;
+    std::vector<uint64_t> beg;
+    ~PieceEvents() {
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+};
+
+// Row pieces of kPiece bytes per slice (measurement option TEC_DEBUG_KNOBS=1 TEC_D2H_PIECE=bytes,
+// 0 = one copy per window as before; TEC_D2H_ROWS=1 copies each piece slice by slice instead of
+// one 2-D copy).  Objects whose slices are shorter than two pieces are copied whole.
+static uint64_t d2h_piece_bytes() {
+    static const uint64_t v = [] {
+        const char *s = tec_knob("TEC_D2H_PIECE");
+        return s ? (uint64_t)strtoull(s, nullptr, 10) : (uint64_t)1 << 20;
+    }();
+    return v;
+}
+static bool d2h_rows() {
+    static const bool v = [] {
+        const char *s = tec_knob("TEC_D2H_ROWS");
+        return s && s[0] == '1';
+    }();
+    return v;
+}
+
+// Page-locked (te_host_alloc / te_host_register / hipHostMalloc): row-piece copies of pageable
+// memory would each go through the driver's staging.
+static bool host_pinned(const void *p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// Copy object o's n slices (slice_len bytes each, at dev / host) out in row pieces on stream s.
+static int copy_out_pieces(uint8_t *host, const uint8_t *dev, uint64_t slice_len, uint32_t n, int device,
+                           hipStream_t s, std::shared_ptr<PieceEvents> &out) {
+    const uint64_t piece = d2h_piece_bytes();
+    auto pe = std::make_shared<PieceEvents>();
+    pe->device = device;
+    for (uint64_t off = 0; off < slice_len;) {
+        const uint64_t w = std::min(piece, slice_len - off);
+        if (d2h_rows()) {
+            for (uint32_t i = 0; i < n; i++)
+                TE_HIP(hipMemcpyAsync(host + i * slice_len + off, dev + i * slice_len + off, w, hipMemcpyDeviceToHost, s));
+        } else {
+            TE_HIP(hipMemcpy2DAsync(host + off, slice_len, dev + off, slice_len, w, n, hipMemcpyDeviceToHost, s));
+        }
+        hipEvent_t e = nullptr;
+        TE_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync));
+        pe->ev.push_back(e);
+        pe->beg.push_back(off);
+        TE_HIP(hipEventRecord(e, s));
+        off += w;
+    }
+    pe->beg.push_back(slice_len);
+    out = std::move(pe);
+    return TE_OK;
+}
+
 // A group's commitment outputs on the device: leaf hashes of row q at q * leaf_b, roots after
 // `rows_cap` rows of leaves, proofs after the roots (rows = objects, in group order).
 struct GroupSeg {
@@ -1791,6 +1858,7 @@ struct GroupSeg {
     std::vector<uint64_t> slice_len, out_bytes;
     const uint8_t *h_out = nullptr;  // the window's host slices (host-hashed groups read them)
     std::vector<uint64_t> h_off;     // per object: its slices at h_out + h_off
+    std::vector<std::shared_ptr<PieceEvents>> pieces;  // per object: row pieces, or null (copied whole)
 };
 struct OpenGroup {
     bool open = false;
@@ -1827,9 +1895,11 @@ static int group_open(CommitPipe &P, OpenGroup &G, uint64_t need_out, uint64_t n
 // of the slices per copy window, rotating over the slot streams.  `last`: the caller's final group
 // -- its encodes run ahead of the copies (one D2H per two encodes on a slot, the rest after the
 // group's last encode), so its hashing, the only exposed one, starts about halfway through the
-// group's copies.
+// group's copies.  `pieces` (a host-hashed group with pinned output): each large object's slices
+// are copied out in row pieces with an event per piece (copy_out_pieces).
 static int group_add(te_clay *c, const te_slicer_cfg *cfg, CommitPipe &P, OpenGroup &G, const CommitBatch &B,
-                     const CommitPlan &L, size_t x, bool last) {
+                     const CommitPlan &L, size_t x, bool last, bool pieces = false) {
+    if (last) pieces = false;
     constexpr int S = CommitPipe::S;
     const size_t i = L.gcut[x], j = L.gcut[x + 1];
     const std::vector<size_t> &wc = L.wcut[x];
@@ -1867,8 +1937,24 @@ static int group_add(te_clay *c, const te_slicer_cfg *cfg, CommitPipe &P, OpenGr
                                  P.arena[k])))
             break;
         if ((rc = hip_status(hipEventRecord(P.ev_enc[k], P.ss[k])))) break;
-        pend[k].push_back(hout);
-        if (!last || ++encs[k] % 2 == 0) {
+        if (pieces) {
+            const uint64_t pb = d2h_piece_bytes();
+            uint64_t od = dout;
+            for (size_t o = a; o < b && !rc; o++) {
+                std::shared_ptr<PieceEvents> pe;
+                if (pb && B.slice_len[o] >= 2 * pb)
+                    rc = copy_out_pieces(B.h_out + B.objs[o].out_off, gout + od, B.slice_len[o], B.n, c->device, P.ss[k], pe);
+                else
+                    rc = hip_status(hipMemcpyAsync(B.h_out + B.objs[o].out_off, gout + od, B.out_bytes[o],
+                                                   hipMemcpyDeviceToHost, P.ss[k]));
+                seg.pieces.push_back(std::move(pe));
+                od += B.out_bytes[o];
+            }
+        } else {
+            pend[k].push_back(hout);
+        }
+        if (rc) break;
+        if (!pieces && (!last || ++encs[k] % 2 == 0)) {
             if ((rc = copy_runs(pend[k].front(), gout, B.h_out, hipMemcpyDeviceToHost, P.ss[k]))) break;
             pend[k].pop_front();
         }
@@ -1947,7 +2033,9 @@ static int group_close_host(CommitPipe &P, OpenGroup &G, uint32_t n, uint32_t he
         return hip_status(e);
     }
     job = std::make_shared<hh::Job>();
-    std::vector<std::function<void()>> tasks;
+    // objects copied out in row pieces hash piece by piece as the pieces land (their tasks go to
+    // the workers at once and wait on the piece events); the rest once the group's copies are done
+    std::vector<std::function<void()>> tasks, streamed;
     const uint32_t lanes = (uint32_t)hh::Pool::get().lanes();
     for (const GroupSeg &sg : G.segs) {
         for (size_t q = 0; q < sg.cnt; q++) {
@@ -1957,9 +2045,10 @@ static int group_close_host(CommitPipe &P, OpenGroup &G, uint32_t n, uint32_t he
             uint8_t *root = sg.co.root + (sg.obj0 + q) * TE_HASH_SIZE;
             uint8_t *proof = sg.co.proof ? sg.co.proof + (sg.obj0 + q) * (uint64_t)n * height * TE_HASH_SIZE : nullptr;
             auto left = std::make_shared<std::atomic<uint32_t>>(n);
-            // one task per `lanes` slices of the object (hash_leaves interleaves them)
+            std::shared_ptr<PieceEvents> pe = q < sg.pieces.size() ? sg.pieces[q] : nullptr;
+            // one task per `lanes` slices of the object (LeafLanes interleaves them)
             for (uint32_t i0 = 0; i0 < n; i0 += lanes)
-                tasks.push_back([=, j = job.get()] {
+                (pe ? streamed : tasks).push_back([=, j = job.get()] {
                     const uint32_t L = std::min(lanes, n - i0);
                     const uint8_t *src[hh::kMaxLanes];
                     uint8_t *dst[hh::kMaxLanes];
@@ -1967,15 +2056,28 @@ static int group_close_host(CommitPipe &P, OpenGroup &G, uint32_t n, uint32_t he
                         src[l] = slices + (uint64_t)(i0 + l) * slen;
                         dst[l] = leaf + (uint64_t)(i0 + l) * TE_HASH_SIZE;
                     }
-                    hh::hash_leaves((int)L, src, slen, dst);
                     int rc = TE_OK;
-                    if (left->fetch_sub(L) == L) rc = host_tree(leaf, n, height, root, proof);
+                    hh::LeafLanes h((int)L);
+                    if (!pe) {
+                        h.update(src, slen);
+                    } else {
+                        (void)hipSetDevice(pe->device);
+                        const uint8_t *at[hh::kMaxLanes];
+                        for (size_t p = 0; p < pe->ev.size() && !rc; p++) {
+                            rc = hip_status(hipEventSynchronize(pe->ev[p]));
+                            for (uint32_t l = 0; l < L; l++) at[l] = src[l] + pe->beg[p];
+                            if (!rc) h.update(at, pe->beg[p + 1] - pe->beg[p]);
+                        }
+                    }
+                    h.final(dst);
+                    if (left->fetch_sub(L) == L && !rc) rc = host_tree(leaf, n, height, root, proof);
                     j->done(rc);
                 });
         }
     }
-    job->add((int64_t)tasks.size());
+    job->add((int64_t)(tasks.size() + streamed.size()));
     G.segs.clear();
+    if (!streamed.empty()) hh::Pool::get().submit_after(nullptr, device, std::move(streamed));
     if (tasks.empty()) {
         (void)hipEventDestroy(landed);
         return TE_OK;
@@ -2146,6 +2248,7 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
     }
     rc = P.make_events();
     const uint64_t row_b = B.leaf_b + TE_HASH_SIZE + B.proof_b;
+    const bool pinned_out = host_pinned(h_out);
     OpenGroup G;
     std::vector<std::shared_ptr<hh::Job>> jobs;
     for (size_t x = 0; x < ngroups && rc == TE_OK; x++) {
@@ -2155,7 +2258,7 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
         for (size_t o = L.gcut[x]; o < L.gcut[x + 1]; o++) max_slice = std::max<uint64_t>(max_slice, B.slice_len[o]);
         const bool host = host_hash_wins(g_commit_hashing.load(), need_rows * B.n, max_slice, need_out);
         rc = group_open(P, G, need_out, need_rows, row_b);
-        if (!rc) rc = group_add(c, cfg, P, G, B, L, x, x + 1 == ngroups && !host);
+        if (!rc) rc = group_add(c, cfg, P, G, B, L, x, x + 1 == ngroups && !host, host && pinned_out);
         if (!rc && host) {
             jobs.emplace_back();
             rc = group_close_host(P, G, B.n, B.co.height, c->device, jobs.back());
@@ -2415,6 +2518,7 @@ int te_stream_submit(te_stream_writer *w, const uint8_t *h_data, const te_object
             slice_bytes += B.out_bytes[o];
         }
         const bool host = host_hash_wins(w->hashing, (uint64_t)nobj * B.n, max_slice, slice_bytes);
+        const bool pinned_out = host && host_pinned(h_out);
         if (d.G.open && d.G_host != host) rc = writer_close(*w, d);
         const uint64_t close_at = std::max<uint64_t>(1, w->group_bytes / 2);
         for (size_t x = 0; x + 1 < L.gcut.size() && !rc; x++) {
@@ -2442,7 +2546,7 @@ int te_stream_submit(te_stream_writer *w, const uint8_t *h_data, const te_object
                 }
                 // on failure the group keeps its earlier segments (group_add adds one only on
                 // success): the earlier windows still complete below
-                if (!rc) rc = group_add(c, &w->cfg, d.P, G, B, L, x, false);
+                if (!rc) rc = group_add(c, &w->cfg, d.P, G, B, L, x, false, host && pinned_out);
             }
             if (!rc && (host || G.bytes >= close_at)) rc = writer_close(*w, d);  // pending windows complete with it
         }

@@ -125,46 +125,66 @@ void blocks(int L, uint32_t *const *st, const uint8_t *const *p, size_t nblocks)
 
 bool have_sha_ext() { return g_sha_ext; }
 
-void hash_leaves(int L, const uint8_t *const *data, size_t len, uint8_t *const *out) {
-    uint32_t state[kMaxLanes][8];
-    uint32_t *st[kMaxLanes];
-    // "LEAF" is the first 4 message bytes: block 0 is assembled, later full blocks are read in
-    // place, the tail (with the padding and the bit length) is assembled again
-    uint8_t b[kMaxLanes][128];
-    const uint8_t *bp[kMaxLanes], *dp[kMaxLanes];
-    const size_t first = len < 60 ? len : 60;
+LeafLanes::LeafLanes(int lanes) : L(lanes) {
     for (int l = 0; l < L; l++) {
-        st[l] = state[l];
-        sha::init(state[l]);
-        memcpy(b[l], "LEAF", 4);
-        if (first) memcpy(b[l] + 4, data[l], first);
-        bp[l] = b[l];
+        sha::init(st[l]);
+        memcpy(buf[l], "LEAF", 4);
     }
-    size_t have = 4 + first, done = first;
-    if (have == 64) {
-        blocks(L, st, bp, 1);
-        const size_t full = (len - done) / 64;
-        for (int l = 0; l < L; l++) dp[l] = data[l] + done;
-        blocks(L, st, dp, full);
-        done += full * 64;
-        for (int l = 0; l < L; l++) memcpy(b[l], data[l] + done, len - done);
-        have = len - done;
+    have = 4;
+}
+
+// Partial blocks are assembled in buf; full blocks are read in place.
+void LeafLanes::update(const uint8_t *const *data, size_t n) {
+    if (n == 0) return;
+    const uint8_t *p[kMaxLanes];
+    uint32_t *sp[kMaxLanes];
+    for (int l = 0; l < L; l++) p[l] = data[l], sp[l] = st[l];
+    len += n;
+    if (have) {
+        const size_t m = std::min(n, 64 - have);
+        for (int l = 0; l < L; l++) memcpy(buf[l] + have, p[l], m), p[l] += m;
+        have += m;
+        n -= m;
+        if (have < 64) return;
+        const uint8_t *bp[kMaxLanes];
+        for (int l = 0; l < L; l++) bp[l] = buf[l];
+        blocks(L, sp, bp, 1);
+        have = 0;
     }
-    const uint64_t bits = (uint64_t)(len + 4) * 8;
+    const size_t full = n / 64;
+    blocks(L, sp, p, full);
+    for (int l = 0; l < L; l++) memcpy(buf[l], p[l] + full * 64, n - full * 64);
+    have = n - full * 64;
+}
+
+void LeafLanes::final(uint8_t *const *out) {
+    const uint64_t bits = (len + 4) * 8;
     const size_t tot = have + 1 + 8 <= 64 ? 64 : 128;
+    uint8_t tail[kMaxLanes][128];
+    const uint8_t *bp[kMaxLanes];
+    uint32_t *sp[kMaxLanes];
     for (int l = 0; l < L; l++) {
-        b[l][have] = 0x80;
-        memset(b[l] + have + 1, 0, tot - 8 - have - 1);
-        for (int i = 0; i < 8; i++) b[l][tot - 8 + i] = (uint8_t)(bits >> (56 - 8 * i));
+        memcpy(tail[l], buf[l], have);
+        tail[l][have] = 0x80;
+        memset(tail[l] + have + 1, 0, tot - 8 - have - 1);
+        for (int i = 0; i < 8; i++) tail[l][tot - 8 + i] = (uint8_t)(bits >> (56 - 8 * i));
+        bp[l] = tail[l];
+        sp[l] = st[l];
     }
-    blocks(L, st, bp, tot / 64);
+    blocks(L, sp, bp, tot / 64);
     for (int l = 0; l < L; l++)
         for (int i = 0; i < 8; i++) {
-            out[l][4 * i] = (uint8_t)(state[l][i] >> 24);
-            out[l][4 * i + 1] = (uint8_t)(state[l][i] >> 16);
-            out[l][4 * i + 2] = (uint8_t)(state[l][i] >> 8);
-            out[l][4 * i + 3] = (uint8_t)state[l][i];
+            out[l][4 * i] = (uint8_t)(st[l][i] >> 24);
+            out[l][4 * i + 1] = (uint8_t)(st[l][i] >> 16);
+            out[l][4 * i + 2] = (uint8_t)(st[l][i] >> 8);
+            out[l][4 * i + 3] = (uint8_t)st[l][i];
         }
+}
+
+void hash_leaves(int L, const uint8_t *const *data, size_t len, uint8_t *const *out) {
+    LeafLanes h(L);
+    h.update(data, len);
+    h.final(out);
 }
 
 void hash_leaf(const uint8_t *data, size_t len, uint8_t out[32]) { hash_leaves(1, &data, len, &out); }

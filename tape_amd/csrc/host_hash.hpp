@@ -33,6 +33,18 @@ void hash_leaf(const uint8_t *data, size_t len, uint8_t out[32]);
 // The same for L <= kMaxLanes messages of one length, interleaved round by round on one thread.
 constexpr int kMaxLanes = 4;
 void hash_leaves(int L, const uint8_t *const *data, size_t len, uint8_t *const *out);
+// Incremental form: the messages arrive in pieces (the same length for every lane per update),
+// e.g. as a window's D2H row pieces land (engine.cpp group_close_host).
+struct LeafLanes {
+    explicit LeafLanes(int lanes);
+    void update(const uint8_t *const *data, size_t n);
+    void final(uint8_t *const *out);
+    int L;
+    uint32_t st[kMaxLanes][8];
+    uint8_t buf[kMaxLanes][64];
+    size_t have = 0;   // bytes in buf
+    uint64_t len = 0;  // message bytes so far ("LEAF" excluded)
+};
 bool have_sha_ext();
 
 // A set of tasks whose completion a ticket waits for.

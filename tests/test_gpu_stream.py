@@ -170,6 +170,21 @@ def test_stream_writer_sdk_chunk_shape(oracle, hashing):
     sw.close()
 
 
+def test_stream_writer_row_pieces_mixed(oracle):
+    """Host-hashed windows into pinned output: objects with slices >= 2 MiB are copied out in 1 MiB
+    row pieces and hashed as the pieces land (the last piece short), smaller ones in one copy hashed
+    after the window's copies -- both kinds in one window, and windows of each kind back to back."""
+    s = T.Slicer.clay_default()
+    sw = batch.StreamWriter([s], hashing="host")
+    wins = [_window(oracle, s, sizes, 60_000 + 11 * k) for k, sizes in enumerate(
+        [[20 * MiB + 7, 4 * MiB, 1000], [15 * MiB], [3 * MiB, 14 * MiB + 1], [0, 1]])]
+    tickets = [sw.submit(w["in"], w["objs"], w["out"], w["leaf"], w["root"], w["proof"]) for w in wins]
+    sw.wait(tickets[-1])
+    for w in wins:
+        _check(oracle, w)
+    sw.close()
+
+
 def test_stream_writer_failed_window_is_isolated(oracle):
     """A window that fails its checks (an object too large for 32-bit slices: TooMuchData) fails
     alone: the windows before it, sharing its device's open hashing group, and after it complete
@@ -196,7 +211,7 @@ def test_host_hashing_one_shot(oracle):
     """te_encode_commit_batch_host with the host pool forced (te_set_commit_hashing): same slices,
     leaves, roots and proofs as the oracle; back to auto afterwards."""
     s = T.Slicer.clay_default()
-    w = _window(oracle, s, [4 * MiB, 1_000_001, 4 * MiB + 8], 4711)
+    w = _window(oracle, s, [4 * MiB, 1_000_001, 4 * MiB + 8, 18 * MiB + 3], 4711)  # the last in row pieces
     batch.set_commit_hashing("host")
     try:
         batch.encode_commit_batch_host(s, w["in"], w["objs"], w["out"], w["leaf"], w["root"], w["proof"])
