@@ -42,7 +42,12 @@ namespace dstage {
 #ifndef TEC_DEC_MAXG
 #define TEC_DEC_MAXG 2  // waves per workgroup at most (direct output: 2 measured best, 6 -> 2: 7.48 -> 5.95 ms)
 #endif
+#ifndef TEC_DEC_TAB_LDS
+#define TEC_DEC_TAB_LDS 1  // 1: the decoding matrix's v_perm tables staged in LDS (broadcast reads); 0: scalar-loaded
+#endif
 constexpr int kMaxG = TEC_DEC_MAXG;
+constexpr uint32_t kTabDw = 8;  // LDS dwords per v_perm table (5 used; 32-byte aligned for one b128 + one b32 read)
+__host__ __device__ constexpr uint32_t tab_lds_bytes(int nk) { return TEC_DEC_TAB_LDS ? (uint32_t)(2 * kRepQ - nk) * nk * kTabDw * 4u : 0u; }
 constexpr uint32_t kMaxLdsRows = 64;  // 2 x staging + zero + trash + slots (G = 6: 96 KB)
 
 // PFT of the supported profiles: U = 3 C ^ 2 Cp = C ^ xt(C ^ Cp), and the inverse has the same
@@ -139,15 +144,35 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
     // depend on nothing and stay in the scalar cache.
     typedef const __attribute__((address_space(4))) PermTab cPermTab;
     cPermTab(*D)[kGpeMaxKnown] = (cPermTab(*)[kGpeMaxKnown])(uintptr_t)(&a.patterns[J.pattern].D[0][0]);
-    const uint32_t *progw = prog[0].w + (lane < kDpWords ? lane : 0u);
-    auto ldw = [&](uint32_t st) -> uint32_t { return progw[st * kDpWords]; };
+    // TEC_DEC_TAB_LDS: the NE x NK tables copied once into LDS after the rows (kTabDw dwords each);
+    // a product then reads its table with one broadcast b128 + b32 LDS read into VGPRs, so the
+    // v_perm needs no v_mov of an SGPR table half (the scalar-loaded form pays 2 per product:
+    // gfx9 VALU reads one SGPR per instruction) and the step waits on no scalar load
+    const uint32_t tab_dw = (a.lds_rows * RS) >> 2;
+    if constexpr (TEC_DEC_TAB_LDS != 0) {
+        const uint32_t *Dw = reinterpret_cast<const uint32_t *>(&a.patterns[J.pattern].D[0][0]);
+        for (uint32_t i = threadIdx.x; i < (uint32_t)(NE * NK * 5); i += G * 64u) {
+            const uint32_t e = i / (NK * 5), r = i - e * (NK * 5), j = r / 5u, t = r - j * 5u;
+            lds[tab_dw + (e * NK + j) * kTabDw + t] = Dw[(e * kGpeMaxKnown + j) * 5u + t];
+        }
+        __syncthreads();
+    }
+    // one 32-bit lane offset into a buffer over the pattern's steps (a per-lane 64-bit pointer
+    // held two more VGPRs across the loop and spilled with the LDS tables)
+    const __amdgpu_buffer_rsrc_t rs_prog = __builtin_amdgcn_make_buffer_rsrc((void *)prog, 0, (int)((H.nsteps + 2) * sizeof(DecStepP)), 0x00020000);
+    const uint32_t progl = (lane < kDpWords ? lane : 0u) * 4u;
+    auto ldw = [&](uint32_t st) -> uint32_t {
+        return __builtin_amdgcn_raw_buffer_load_b32(rs_prog, (int)progl, (int)(st * (uint32_t)sizeof(DecStepP)), 0);
+    };
     auto W = [](uint32_t v, int i) -> uint32_t { return __builtin_amdgcn_readlane(v, i); };
     const bool kd_l = lane >= kDpKd && lane < kDpKd + NK, ed_l = lane >= kDpEd && lane < kDpEd + NE;
     // input offset of the partner load word x describes (known input partner, type-1 partner)
     auto vec_in = [&](uint32_t x) -> uint32_t {
         const uint32_t k = x >> 28;
         const bool on = (kd_l && k == kKnInput) || (ed_l && k == kErType1);
-        const uint32_t sl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((x & 0xffu) << 2), (int)sl_lane);
+        uint32_t sl_l = lane + J.rot;  // sl_lane, recomputed (not held across the loop)
+        sl_l = (sl_l >= a.n ? sl_l - a.n : sl_l) * (uint32_t)a.in_stride;
+        const uint32_t sl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((x & 0xffu) << 2), (int)sl_l);
         return on ? sl + ((x >> 8) & 0xffu) * sc : kDrop;
     };
     // a consumed location (known partner C, pair partner U): scratch offset or kDrop ...
@@ -280,6 +305,21 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
             // known inputs in pairs: 3 perms and 1.5 XOR3 per product, plus a v_mov per 3-bit perm
             // when both table halves are SGPRs (one SGPR operand per VALU instruction on gfx9; the
             // tables in LDS instead, one broadcast ds_read_b128 per product, measured 30 % slower)
+            if constexpr (TEC_DEC_TAB_LDS != 0) {
+                const uint32_t *tr = lds + tab_dw + (uint32_t)e * NK * kTabDw;
+                auto tq = [&](int j) { return *reinterpret_cast<const u32x4 *>(tr + j * kTabDw); };
+#pragma unroll
+                for (int j = 0; j + 1 < NK; j += 2) {
+                    const u32x4 p = tq(j), q = tq(j + 1);
+                    acc[e] = perm_mul2_acc(acc[e], sel[j], p.x, p.y, p.z, p.w, tr[j * kTabDw + 4], sel[j + 1], q.x, q.y, q.z,
+                                           q.w, tr[(j + 1) * kTabDw + 4]);
+                }
+                if (NK & 1) {
+                    const u32x4 p = tq(NK - 1);
+                    acc[e] = perm_mul_acc(acc[e], sel[NK - 1], p.x, p.y, p.z, p.w, tr[(NK - 1) * kTabDw + 4]);
+                }
+                continue;
+            }
 #pragma unroll
             for (int j = 0; j + 1 < NK; j += 2)
                 acc[e] = perm_mul2_acc(acc[e], sel[j], D[e][j].t[0], D[e][j].t[1], D[e][j].t[2], D[e][j].t[3], D[e][j].t[4],
@@ -374,7 +414,7 @@ size_t decode_stage_scratch_bytes(const DecArgs &a) {
 
 template <int NK, int G>
 static hipError_t launch_dec_g(const DecArgs &a, uint64_t blocks, hipStream_t s) {
-    const size_t lds = (size_t)a.lds_rows * G * 256u;
+    const size_t lds = (size_t)a.lds_rows * G * 256u + dstage::tab_lds_bytes(NK);
     hipError_t e = ensure_dyn_lds(reinterpret_cast<const void *>(dstage::dec_stage_kernel<NK, G>), lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((dstage::dec_stage_kernel<NK, G>), dim3((uint32_t)blocks), dim3(G * 64), lds, s, a);
