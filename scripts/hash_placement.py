@@ -84,13 +84,31 @@ def run(cpus, bufs, lanes):
     return sum(done) / (time.perf_counter() - t) / 1e9
 
 
+def page_node(addr):
+    """NUMA node of the page at addr (get_mempolicy(MPOL_F_NODE | MPOL_F_ADDR)), or -1."""
+    libc = C.CDLL(None, use_errno=True)
+    mode = C.c_int(-1)
+    r = libc.syscall(239, C.byref(mode), None, C.c_ulong(0), C.c_void_p(addr), C.c_ulong(3))  # SYS_get_mempolicy
+    return mode.value if r == 0 else -1
+
+
 def main():
     info = topo()
     lanes = lib.te_host_hash_lanes()
     rng = np.random.default_rng(1)
-    bufs = [rng.integers(0, 256, N * SL, dtype=np.uint8) for _ in range(NT)]
-    res = {"threads": NT, "lanes": lanes, "affinity_cpus": len(info),
+    kind = os.environ.get("BUF", "pageable")
+    if kind == "pinned":  # te_host_alloc (hipHostMalloc, portable), as the stream writer's buffers
+        from tape_amd import batch
+        bufs = []
+        for _ in range(NT):
+            b = batch.host_empty(N * SL)
+            b[:] = rng.integers(0, 256, N * SL, dtype=np.uint8)
+            bufs.append(b)
+    else:
+        bufs = [rng.integers(0, 256, N * SL, dtype=np.uint8) for _ in range(NT)]
+    res = {"threads": NT, "lanes": lanes, "buffers": kind, "affinity_cpus": len(info),
            "numa_nodes": sorted({v[2] for v in info.values()}),
+           "buffer_nodes": sorted({page_node(b.ctypes.data + i * (1 << 21)) for b in bufs for i in range(0, 90, 30)}),
            "one_thread_GBps": None, "GBps": {}}
     res["one_thread_GBps"] = round(run_one(bufs[0], lanes), 3)
     for name, cpus in policies(info).items():

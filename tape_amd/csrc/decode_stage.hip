@@ -43,7 +43,7 @@ namespace dstage {
 #define TEC_DEC_MAXG 2  // waves per workgroup at most (direct output: 2 measured best, 6 -> 2: 7.48 -> 5.95 ms)
 #endif
 #ifndef TEC_DEC_TAB_LDS
-#define TEC_DEC_TAB_LDS 1  // 1: the decoding matrix's v_perm tables staged in LDS (broadcast reads); 0: scalar-loaded
+#define TEC_DEC_TAB_LDS 0  // 1: v_perm tables staged in LDS (broadcast reads; r04 A/B: random 5.52 vs 5.51 ms, recover 4.12 vs 3.93); 0: scalar-loaded
 #endif
 constexpr int kMaxG = TEC_DEC_MAXG;
 constexpr uint32_t kTabDw = 8;  // LDS dwords per v_perm table (5 used; 32-byte aligned for one b128 + one b32 read)

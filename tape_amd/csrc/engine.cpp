@@ -2352,7 +2352,9 @@ int writer_close(te_stream_writer &w, te_stream_writer::Dev &d) {
         if (!rc) {
             // after the group's hashing and copies (a ticket spanning several groups re-records)
             DeviceGuard dg(d.device);
-            if (!T.done) rc = hip_status(hipEventCreateWithFlags(&T.done, hipEventDisableTiming));
+            // blocking: te_stream_wait sleeps in hipEventSynchronize instead of spinning a core the
+            // host hashing pool could use (the GPU's host share is 16 CPUs of time on the pool)
+            if (!T.done) rc = hip_status(hipEventCreateWithFlags(&T.done, hipEventDisableTiming | hipEventBlockingSync));
             if (!rc) rc = hip_status(hipEventRecord(T.done, d.hs));
         }
         if (job) T.jobs.push_back(job);
