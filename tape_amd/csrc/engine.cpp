@@ -60,6 +60,19 @@ int hip_status(hipError_t e) {
         if (e_ != hipSuccess) return hip_status(e_); \
     } while (0)
 
+// Wait for the work queued on s so far by sleeping on a blocking-sync event, not spinning in
+// hipStreamSynchronize: a caller that waits while the host hashing pool runs must not take one of
+// the process's CPUs (the GPU's host share is a 16-CPU quota on the pool this runs on).
+int sync_sleep(hipStream_t s) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess)
+        return hip_status(hipStreamSynchronize(s));
+    hipError_t r = hipEventRecord(e, s);
+    if (r == hipSuccess) r = hipEventSynchronize(e);
+    (void)hipEventDestroy(e);
+    return hip_status(r);
+}
+
 int g_device_count = -1;
 std::mutex g_dev_mu;
 
@@ -2267,10 +2280,10 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
         }
     }
     for (int k = 0; k < CommitPipe::S; k++) {
-        const int r2 = hip_status(hipStreamSynchronize(P.ss[k]));
+        const int r2 = sync_sleep(P.ss[k]);
         if (rc == TE_OK) rc = r2;
     }
-    const int r2 = hip_status(hipStreamSynchronize(P.hs));
+    const int r2 = sync_sleep(P.hs);
     if (rc == TE_OK) rc = r2;
     for (auto &j : jobs) {  // host-hashed groups: their tasks read the output buffers
         const int r3 = j ? j->wait() : TE_OK;
@@ -2369,11 +2382,11 @@ int writer_drain(te_stream_writer::Dev &d) {
     int rc = TE_OK;
     for (int k = 0; k < CommitPipe::S; k++)
         if (d.ss[k]) {
-            const int r = hip_status(hipStreamSynchronize(d.ss[k]));
+            const int r = sync_sleep(d.ss[k]);
             if (!rc) rc = r;
         }
     if (d.hs) {
-        const int r = hip_status(hipStreamSynchronize(d.hs));
+        const int r = sync_sleep(d.hs);
         if (!rc) rc = r;
     }
     return rc;
