@@ -439,7 +439,8 @@ int te_outer_encode_device(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t
 /* Device form of the decode (outer.rs:126-197) for snapshot reads: d_chunks = n DEVICE pointers
  * (host array; NULL = missing), each chunk_bytes long; d_out = the k data chunks (DEVICE,
  * k * chunk_bytes).  Received data chunks are copied, missing ones restored from the first k
- * received chunks on the GPU.  Runs on hip_stream and waits for it. */
+ * received chunks on the GPU.  Enqueued on hip_stream; returns without waiting (the d_chunks
+ * array is read before it returns).  The decoding tables are cached per erasure pattern. */
 int te_outer_decode_device(uint32_t k, uint32_t n, const uint8_t *const *d_chunks, uint64_t chunk_bytes,
                            uint8_t *d_out, void *hip_stream);
 

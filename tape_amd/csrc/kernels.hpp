@@ -268,9 +268,9 @@ struct Rs16EncArgs {
     uint32_t one_chunk;         // low rate, c <= 32: one chunk of work in LDS, the IFFT kept in registers
 };
 struct Rs16DecArgs {
-    const uint8_t *const *recv; // k received shards (device pointer array)
-    uint8_t *const *out;        // nmiss restored originals
-    const uint16_t *lut;        // nmiss x k nibble tables (decoding-matrix coefficients)
+    const uint8_t *recv[kRs16MaxK]; // k received shards (kernel arguments: nothing to upload per call)
+    uint8_t *out[kRs16MaxK];        // nmiss restored originals
+    const uint16_t *lut;            // nmiss x k nibble tables (decoding-matrix coefficients)
     uint32_t k, nmiss, elems;
 };
 hipError_t launch_rs16_encode(const Rs16EncArgs &a, uint32_t segments, hipStream_t s);

@@ -17,6 +17,9 @@ namespace tec {
 namespace rs16k {
 
 constexpr uint32_t kRs16DecLds = 48 * 1024;  // decoding tables staged in LDS up to this size
+#ifndef TEC_RS16_UNROLL
+#define TEC_RS16_UNROLL 1  // butterfly groups in flight per thread in the transforms' inner loops
+#endif
 
 __device__ __forceinline__ uint32_t mulx(uint32_t x, const uint16_t *T) {
     return T[x & 15u] ^ T[16u + ((x >> 4) & 15u)] ^ T[32u + ((x >> 8) & 15u)] ^ T[48u + (x >> 12)];
@@ -38,6 +41,7 @@ __device__ void fft(const Col &c, const uint16_t *lut, uint32_t pos, uint32_t si
         for (uint32_t r = 0; r < trunc; r += dist4) {
             const uint32_t b = r + dist + delta - 1;
             const uint16_t *t0 = lut + b * 64u, *t1 = lut + (b + dist) * 64u, *t2 = lut + (b + 2 * dist) * 64u;
+#pragma unroll TEC_RS16_UNROLL
             for (uint32_t i = r; i < r + dist; i++) {
                 const uint32_t p = pos + i;
                 uint32_t x0 = c.ld(p), x1 = c.ld(p + dist), x2 = c.ld(p + 2 * dist), x3 = c.ld(p + 3 * dist);
@@ -71,6 +75,7 @@ __device__ void ifft(const Col &c, const uint16_t *lut, uint32_t pos, uint32_t s
         for (uint32_t r = 0; r < trunc; r += dist4) {
             const uint32_t b = r + dist + delta - 1;
             const uint16_t *t0 = lut + b * 64u, *t1 = lut + (b + dist) * 64u, *t2 = lut + (b + 2 * dist) * 64u;
+#pragma unroll TEC_RS16_UNROLL
             for (uint32_t i = r; i < r + dist; i++) {
                 const uint32_t p = pos + i;
                 uint32_t x0 = c.ld(p), x1 = c.ld(p + dist), x2 = c.ld(p + 2 * dist), x3 = c.ld(p + 3 * dist);
@@ -173,37 +178,69 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(TEC_R
 // coefficient, staged in LDS).  REG (k <= 32): a thread loads its element of each received shard
 // once into registers and computes every missing output from them (the first kernel re-read the
 // k received elements for each of the nmiss outputs).
-template <bool REG>
+// TLDS: the tables staged in LDS (<= kRs16DecLds), else read from L2.  A compile-time choice, so the
+// lookups are ds_read_u16 with 32-bit addresses: a run-time select between the two pointers made
+// every lookup a flat load with 64-bit address arithmetic (r04: 1,225 flat loads and 4,577 VALU per
+// wave per segment, 16 VALU per product)
+template <int KB, bool TLDS>  // KB: k rounded up to 4 (<= 32), 0 = any k, elements re-read per output
 __global__ void __launch_bounds__(512) rs16_decode_kernel(Rs16DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lds16[];
     const uint32_t ntab = a.nmiss * a.k;
-    const bool in_lds = ntab * 128u <= kRs16DecLds;  // else the tables are read from L2
-    if (in_lds) {
+    if constexpr (TLDS) {
         for (uint32_t t = threadIdx.x; t < ntab * 32u; t += blockDim.x)
             reinterpret_cast<uint32_t *>(lds16)[t] = reinterpret_cast<const uint32_t *>(a.lut)[t];
         __syncthreads();
     }
-    const uint16_t *tab = in_lds ? lds16 : a.lut;
+    const uint16_t *tab;
+    if constexpr (TLDS) tab = lds16; else tab = a.lut;
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= a.elems) return;
-    if constexpr (REG) {
-        uint32_t x[16];  // received elements, two per register
+    if constexpr (KB > 0) {
+        // two adjacent elements per thread (their low bytes adjacent, their high bytes 32 B on:
+        // 16-bit loads and stores instead of byte ones).  Per received element its four lookup
+        // offsets into a coefficient's 64-entry table, one byte each (byte q = 32 q + 2 * nibble
+        // q), built once: a lookup is then one add with a byte select plus the ds_read (the r02
+        // kernel re-derived each nibble index per output).  KB = k rounded up to 4: the products
+        // run branch-free (a branch per product kept each product's four reads waiting alone);
+        // the r >= k ones read entry 0 (= 0) of table k - 1
+        const uint32_t e0 = 2u * e;
+        if (e0 >= a.elems) return;
+        const uint32_t eo = (e0 >> 5) * 64u + (e0 & 31u);  // e0 even: 2-byte aligned
+        auto spread = [](uint32_t x) {
+            return ((x & 0xfu) << 1) | ((x & 0xf0u) << 5) | ((x & 0xf00u) << 9) | ((x & 0xf000u) << 13) | 0x60402000u;
+        };
+        uint32_t off0[KB], off1[KB];
 #pragma unroll
-        for (uint32_t q = 0; q < 16u; q++)
-            x[q] = (2 * q < a.k ? ld_elem(a.recv[2 * q], e) : 0u) | (2 * q + 1 < a.k ? ld_elem(a.recv[2 * q + 1], e) << 16 : 0u);
+        for (uint32_t r = 0; r < (uint32_t)KB; r++) {
+            uint32_t lo = 0, hi = 0;
+            if (r < a.k) {
+                lo = *reinterpret_cast<const uint16_t *>(a.recv[r] + eo);
+                hi = *reinterpret_cast<const uint16_t *>(a.recv[r] + eo + 32u);
+            }
+            off0[r] = spread((lo & 0xffu) | (hi & 0xffu) << 8);
+            off1[r] = spread((lo >> 8) | (hi & 0xff00u));
+        }
 #pragma unroll 1
         for (uint32_t i = 0; i < a.nmiss; i++) {
-            const uint16_t *t = tab + i * a.k * 64u;
-            uint32_t acc = 0;
+            const uint8_t *ti = reinterpret_cast<const uint8_t *>(tab) + i * a.k * 128u;
 #pragma unroll
-            for (uint32_t q = 0; q < 16u; q++) asm volatile("" : "+v"(x[q]));  // keep the nibble
-            // indices inside the loop (hoisted, 128 of them spilled)
+            for (uint32_t r = 0; r < (uint32_t)KB; r++) asm volatile("" : "+v"(off0[r]), "+v"(off1[r]));  // packed
+            uint32_t acc0 = 0, acc1 = 0;
+            auto look = [](const uint8_t *tr, uint32_t o) {
+                return *reinterpret_cast<const uint16_t *>(tr + (o & 0xffu)) ^
+                       *reinterpret_cast<const uint16_t *>(tr + ((o >> 8) & 0xffu)) ^
+                       *reinterpret_cast<const uint16_t *>(tr + ((o >> 16) & 0xffu)) ^
+                       *reinterpret_cast<const uint16_t *>(tr + (o >> 24));
+            };
 #pragma unroll
-            for (uint32_t q = 0; q < 16u; q++) {
-                if (2 * q < a.k) acc ^= mulx(x[q] & 0xffffu, t + 2 * q * 64u);
-                if (2 * q + 1 < a.k) acc ^= mulx(x[q] >> 16, t + (2 * q + 1) * 64u);
+            for (uint32_t r = 0; r < (uint32_t)KB; r++) {
+                const uint8_t *tr = ti + (r < a.k ? r : a.k - 1u) * 128u;
+                acc0 ^= look(tr, off0[r]);
+                acc1 ^= look(tr, off1[r]);
             }
-            st_elem(a.out[i], e, acc);
+            uint8_t *o = a.out[i] + eo;
+            *reinterpret_cast<uint16_t *>(o) = (uint16_t)((acc0 & 0xffu) | (acc1 & 0xffu) << 8);
+            *reinterpret_cast<uint16_t *>(o + 32u) = (uint16_t)((acc0 >> 8) | (acc1 & 0xff00u));
         }
     } else {
         for (uint32_t i = 0; i < a.nmiss; i++) {
@@ -212,6 +249,20 @@ __global__ void __launch_bounds__(512) rs16_decode_kernel(Rs16DecArgs a) {
             st_elem(a.out[i], e, acc);
         }
     }
+}
+
+// k <= 32: the KB = ceil(k / 4) * 4 instance; larger k: elements re-read per output
+template <int KB>
+hipError_t launch_dec_kb(const Rs16DecArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
+    if constexpr (KB <= 32) {
+        if (a.k > (uint32_t)KB) return launch_dec_kb<KB + 4>(a, grid, block, lds, s);
+        if (lds) hipLaunchKernelGGL((rs16_decode_kernel<KB, true>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((rs16_decode_kernel<KB, false>), grid, block, 0, s, a);
+    } else {
+        if (lds) hipLaunchKernelGGL((rs16_decode_kernel<0, true>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((rs16_decode_kernel<0, false>), grid, block, 0, s, a);
+    }
+    return hipGetLastError();
 }
 
 }  // namespace rs16k
@@ -253,11 +304,12 @@ hipError_t launch_rs16_decode(const Rs16DecArgs &a, hipStream_t s) {
     if (a.elems == 0 || a.nmiss == 0) return hipSuccess;
     const size_t tab = (size_t)a.nmiss * a.k * 128u, lds = tab <= rs16k::kRs16DecLds ? tab : 0;
     if (a.k > kRs16MaxK || a.nmiss > kRs16MaxK) return hipErrorInvalidValue;
-    // 512-thread blocks: the tables (<= 48 KB) are staged once per 8 waves, not per 2
-    const dim3 grid((uint32_t)((a.elems + 511) / 512)), block(512);
-    if (a.k <= 32) hipLaunchKernelGGL(rs16k::rs16_decode_kernel<true>, grid, block, lds, s, a);
-    else hipLaunchKernelGGL(rs16k::rs16_decode_kernel<false>, grid, block, lds, s, a);
-    return hipGetLastError();
+    // 512-thread blocks: the tables (<= 48 KB) are staged once per 8 waves, not per 2; k <= 32:
+    // two elements per thread (elems is a multiple of 32: 64-byte shard blocks)
+    if (a.k <= 32 && a.elems % 2) return hipErrorInvalidValue;
+    const uint64_t threads = a.k <= 32 ? a.elems / 2 : a.elems;
+    const dim3 grid((uint32_t)((threads + 511) / 512)), block(512);
+    return rs16k::launch_dec_kb<4>(a, grid, block, lds, s);
 }
 
 }  // namespace tec
