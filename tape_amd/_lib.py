@@ -182,6 +182,7 @@ def _load() -> C.CDLL:
         "te_outer_decode": (i, [u32, u32, pp, sz, u8p, sz]),
         "te_outer_encode_device": (i, [u32, u32, vp, u64, u32, u64, vp, u64, vp]),
         "te_outer_decode_device": (i, [u32, u32, pp, u64, vp, vp]),
+        "te_outer_decode_device_batch": (i, [u32, u32, pp, u32, u64, vp, u64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -3632,15 +3632,15 @@ int te_outer_decode(uint32_t k, uint32_t n, const uint8_t *const *chunks, size_t
     TE_HIP(hipMalloc((void **)&d, sh + rs));
     Rs16DecArgs a{};
     for (uint32_t j = 0; j < k && r == TE_OK; j++) {
-        a.recv[j] = d + (size_t)j * chunk_bytes;
+        a.ptr[j] = d + (size_t)j * chunk_bytes;
         r = hip_status(hipMemcpy(d + (size_t)j * chunk_bytes, chunks[recv[j]], chunk_bytes, hipMemcpyHostToDevice));
     }
-    for (uint32_t i = 0; i < nm; i++) a.out[i] = d + sh + (size_t)i * chunk_bytes;
+    for (uint32_t i = 0; i < nm; i++) a.ptr[k + i] = d + sh + (size_t)i * chunk_bytes;
     if (r == TE_OK) {
         a.lut = L->d;
         a.k = k; a.nmiss = nm; a.elems = (uint32_t)(chunk_bytes / 2);
         KTimer kt(nullptr);
-        r = hip_status(launch_rs16_decode(a, nullptr));
+        r = hip_status(launch_rs16_decode(a, 1, nullptr));
         kt.stop();
         if (r == TE_OK) r = hip_status(hipEventRecord(L->used, nullptr));
     }
@@ -3651,45 +3651,87 @@ int te_outer_decode(uint32_t k, uint32_t n, const uint8_t *const *chunks, size_t
     return r;
 }
 
-int te_outer_decode_device(uint32_t k, uint32_t n, const uint8_t *const *d_chunks, uint64_t chunk_bytes,
-                           uint8_t *d_out, void *stream) {
-    if (k == 0 || k > n || !d_chunks || !d_out) return TE_ERR_INVALID_ARG;
-    std::vector<uint32_t> have;
-    for (uint32_t i = 0; i < n; i++)
-        if (d_chunks[i]) have.push_back(i);
-    if (have.size() < k) return TE_ERR_NOT_ENOUGH_SLICES;   // outer.rs:127-129
+}  // extern "C"
+
+namespace {
+// OuterCoder decode of `segments` segments on the device (outer.rs:126-197 per segment): segment g's
+// chunk i at d_chunks[g * n + i] (NULL = missing), its k data chunks to d_out + g * seg_out.
+// Received data chunks are copied; segments are grouped by erasure pattern, and each group's
+// missing chunks are restored from its first k received chunks in launches of as many segments
+// as fit the kernel's pointer arguments.  Enqueued on the stream, nothing uploaded but a new
+// pattern's tables (cached): a snapshot read's segments queue back to back (r04: a host wait per
+// segment cost 0.19 ms per 0.2 ms kernel).
+int outer_decode_segs(uint32_t k, uint32_t n, const uint8_t *const *d_chunks, uint32_t segments, uint64_t chunk_bytes,
+                      uint8_t *d_out, uint64_t seg_out, hipStream_t s) {
+    if (k == 0 || k > n || !d_chunks || !d_out || segments == 0) return TE_ERR_INVALID_ARG;
     const uint32_t m = n - k;
-    std::vector<uint32_t> miss;
-    for (uint32_t i = 0; i < k; i++)
-        if (!d_chunks[i]) miss.push_back(i);
-    if (!miss.empty() && m == 0) return TE_ERR_INVALID_LAYOUT;  // outer.rs:143-152
     if (chunk_bytes == 0 || chunk_bytes % 64 || chunk_bytes / 2 > 0xffffffffull) return TE_ERR_INVALID_LAYOUT;
-    if (!miss.empty() && (rs16::use_high_rate(k, m) < 0 || k > kRs16MaxK)) return TE_ERR_UNSUPPORTED;
+    // validate every segment before anything is enqueued
+    std::map<std::vector<uint32_t>, std::vector<uint32_t>> groups;  // recv | miss -> segments
+    for (uint32_t g = 0; g < segments; g++) {
+        const uint8_t *const *ch = d_chunks + (size_t)g * n;
+        std::vector<uint32_t> have, miss;
+        for (uint32_t i = 0; i < n; i++)
+            if (ch[i]) have.push_back(i);
+        if (have.size() < k) return TE_ERR_NOT_ENOUGH_SLICES;   // outer.rs:127-129
+        for (uint32_t i = 0; i < k; i++)
+            if (!ch[i]) miss.push_back(i);
+        if (miss.empty()) continue;
+        if (m == 0) return TE_ERR_INVALID_LAYOUT;  // outer.rs:143-152
+        if (rs16::use_high_rate(k, m) < 0 || k > kRs16MaxK || k + miss.size() > kRs16DecPtrs) return TE_ERR_UNSUPPORTED;
+        std::vector<uint32_t> key(have.begin(), have.begin() + k);  // any k shards determine the originals
+        key.push_back(0xffffffffu);
+        key.insert(key.end(), miss.begin(), miss.end());
+        groups[key].push_back(g);
+    }
     if (device_count() <= 0) return TE_ERR_NO_DEVICE;
-    hipStream_t s = (hipStream_t)stream;
     int r = TE_OK;
-    for (uint32_t i = 0; i < k && r == TE_OK; i++)
-        if (d_chunks[i]) r = hip_status(hipMemcpyAsync(d_out + (size_t)i * chunk_bytes, d_chunks[i], chunk_bytes, hipMemcpyDeviceToDevice, s));
-    if (r != TE_OK || miss.empty()) return r;
-    std::vector<uint32_t> recv(have.begin(), have.begin() + k);  // any k shards determine the originals
-    const uint32_t nm = (uint32_t)miss.size();
+    for (uint32_t g = 0; g < segments && r == TE_OK; g++)
+        for (uint32_t i = 0; i < k && r == TE_OK; i++)
+            if (const uint8_t *c = d_chunks[(size_t)g * n + i])
+                r = hip_status(hipMemcpyAsync(d_out + g * seg_out + (size_t)i * chunk_bytes, c, chunk_bytes,
+                                              hipMemcpyDeviceToDevice, s));
+    if (r != TE_OK || groups.empty()) return r;
     int dev = 0;
     TE_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(g_outer_mu);
-    OuterLut *L = nullptr;
-    if ((r = outer_lut(k, m, recv, miss, dev, L))) return r;
-    // the shard pointers travel as kernel arguments: nothing is uploaded per call
-    Rs16DecArgs a{};
-    for (uint32_t j = 0; j < k; j++) a.recv[j] = d_chunks[recv[j]];
-    for (uint32_t i = 0; i < nm; i++) a.out[i] = d_out + (size_t)miss[i] * chunk_bytes;
-    a.lut = L->d;
-    a.k = k; a.nmiss = nm; a.elems = (uint32_t)(chunk_bytes / 2);
-    KTimer kt(s);
-    r = hip_status(launch_rs16_decode(a, s));
-    kt.stop();
-    if (r == TE_OK) r = hip_status(hipEventRecord(L->used, s));
-    return r;  // enqueued: a snapshot read's segments queue back to back (r04: a wait per call cost
-               // 0.19 ms of host time per 0.2 ms segment)
+    for (const auto &gr : groups) {
+        const auto sep = std::find(gr.first.begin(), gr.first.end(), 0xffffffffu);
+        const std::vector<uint32_t> recv(gr.first.begin(), sep), miss(sep + 1, gr.first.end());
+        const uint32_t nm = (uint32_t)miss.size(), per = k + nm, fit = kRs16DecPtrs / per;
+        OuterLut *L = nullptr;
+        if ((r = outer_lut(k, m, recv, miss, dev, L))) return r;
+        for (size_t g0 = 0; g0 < gr.second.size(); g0 += fit) {
+            const uint32_t cnt = (uint32_t)std::min<size_t>(fit, gr.second.size() - g0);
+            Rs16DecArgs a{};
+            for (uint32_t q = 0; q < cnt; q++) {
+                const uint32_t g = gr.second[g0 + q];
+                for (uint32_t j = 0; j < k; j++) a.ptr[q * per + j] = d_chunks[(size_t)g * n + recv[j]];
+                for (uint32_t i = 0; i < nm; i++) a.ptr[q * per + k + i] = d_out + g * seg_out + (size_t)miss[i] * chunk_bytes;
+            }
+            a.lut = L->d;
+            a.k = k; a.nmiss = nm; a.elems = (uint32_t)(chunk_bytes / 2);
+            KTimer kt(s);
+            r = hip_status(launch_rs16_decode(a, cnt, s));
+            kt.stop();
+            if (r) return r;
+        }
+        if ((r = hip_status(hipEventRecord(L->used, s)))) return r;
+    }
+    return r;
+}
+}  // namespace
+
+extern "C" {
+
+int te_outer_decode_device(uint32_t k, uint32_t n, const uint8_t *const *d_chunks, uint64_t chunk_bytes,
+                           uint8_t *d_out, void *stream) {
+    return outer_decode_segs(k, n, d_chunks, 1, chunk_bytes, d_out, 0, (hipStream_t)stream);
+}
+
+int te_outer_decode_device_batch(uint32_t k, uint32_t n, const uint8_t *const *d_chunks, uint32_t segments,
+                                 uint64_t chunk_bytes, uint8_t *d_out, uint64_t seg_out, void *stream) {
+    return outer_decode_segs(k, n, d_chunks, segments, chunk_bytes, d_out, seg_out, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -267,14 +267,16 @@ struct Rs16EncArgs {
     uint32_t k, m, c, high, work_len, span, elems;  // elems: field elements per shard (bytes / 2)
     uint32_t one_chunk;         // low rate, c <= 32: one chunk of work in LDS, the IFFT kept in registers
 };
+constexpr uint32_t kRs16DecPtrs = 256;  // shard pointers per decode launch (kernel arguments)
 struct Rs16DecArgs {
-    const uint8_t *recv[kRs16MaxK]; // k received shards (kernel arguments: nothing to upload per call)
-    uint8_t *out[kRs16MaxK];        // nmiss restored originals
+    // per segment g (grid.y): its k received shards at ptr[g * (k + nmiss) + r], then its nmiss
+    // restored originals -- kernel arguments, so a call uploads nothing
+    const uint8_t *ptr[kRs16DecPtrs];
     const uint16_t *lut;            // nmiss x k nibble tables (decoding-matrix coefficients)
     uint32_t k, nmiss, elems;
 };
 hipError_t launch_rs16_encode(const Rs16EncArgs &a, uint32_t segments, hipStream_t s);
-hipError_t launch_rs16_decode(const Rs16DecArgs &a, hipStream_t s);
+hipError_t launch_rs16_decode(const Rs16DecArgs &a, uint32_t segments, hipStream_t s);
 hipError_t launch_repair(const RepArgs &a, uint32_t max_erased, hipStream_t s);
 hipError_t launch_repair_stage(RepArgs a, hipStream_t s);
 // repair_fold.hip: Clay(20,7,16) with minimum_to_repair's helper set when at most one of the

@@ -195,6 +195,9 @@ __global__ void __launch_bounds__(512) rs16_decode_kernel(Rs16DecArgs a) {
     if constexpr (TLDS) tab = lds16; else tab = a.lut;
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= a.elems) return;
+    const uint32_t pb = blockIdx.y * (a.k + a.nmiss);
+    auto recv = [&](uint32_t r) { return a.ptr[pb + r]; };
+    auto outp = [&](uint32_t i) { return const_cast<uint8_t *>(a.ptr[pb + a.k + i]); };
     if constexpr (KB > 0) {
         // two adjacent elements per thread (their low bytes adjacent, their high bytes 32 B on:
         // 16-bit loads and stores instead of byte ones).  Per received element its four lookup
@@ -214,8 +217,8 @@ __global__ void __launch_bounds__(512) rs16_decode_kernel(Rs16DecArgs a) {
         for (uint32_t r = 0; r < (uint32_t)KB; r++) {
             uint32_t lo = 0, hi = 0;
             if (r < a.k) {
-                lo = *reinterpret_cast<const uint16_t *>(a.recv[r] + eo);
-                hi = *reinterpret_cast<const uint16_t *>(a.recv[r] + eo + 32u);
+                lo = *reinterpret_cast<const uint16_t *>(recv(r) + eo);
+                hi = *reinterpret_cast<const uint16_t *>(recv(r) + eo + 32u);
             }
             off0[r] = spread((lo & 0xffu) | (hi & 0xffu) << 8);
             off1[r] = spread((lo >> 8) | (hi & 0xff00u));
@@ -238,22 +241,22 @@ __global__ void __launch_bounds__(512) rs16_decode_kernel(Rs16DecArgs a) {
                 acc0 ^= look(tr, off0[r]);
                 acc1 ^= look(tr, off1[r]);
             }
-            uint8_t *o = a.out[i] + eo;
+            uint8_t *o = outp(i) + eo;
             *reinterpret_cast<uint16_t *>(o) = (uint16_t)((acc0 & 0xffu) | (acc1 & 0xffu) << 8);
             *reinterpret_cast<uint16_t *>(o + 32u) = (uint16_t)((acc0 >> 8) | (acc1 & 0xff00u));
         }
     } else {
         for (uint32_t i = 0; i < a.nmiss; i++) {
             uint32_t acc = 0;
-            for (uint32_t r = 0; r < a.k; r++) acc ^= mulx(ld_elem(a.recv[r], e), tab + (i * a.k + r) * 64u);
-            st_elem(a.out[i], e, acc);
+            for (uint32_t r = 0; r < a.k; r++) acc ^= mulx(ld_elem(recv(r), e), tab + (i * a.k + r) * 64u);
+            st_elem(outp(i), e, acc);
         }
     }
 }
 
 // k <= 32: the KB = ceil(k / 4) * 4 instance; larger k: elements re-read per output
 template <int KB>
-hipError_t launch_dec_kb(const Rs16DecArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
+hipError_t launch_dec_kb(const Rs16DecArgs &a, dim3 grid, dim3 block, size_t lds, hipStream_t s) {  // grid.y = segments
     if constexpr (KB <= 32) {
         if (a.k > (uint32_t)KB) return launch_dec_kb<KB + 4>(a, grid, block, lds, s);
         if (lds) hipLaunchKernelGGL((rs16_decode_kernel<KB, true>), grid, block, lds, s, a);
@@ -300,15 +303,16 @@ hipError_t launch_rs16_encode(const Rs16EncArgs &a, uint32_t segments, hipStream
     return hipGetLastError();
 }
 
-hipError_t launch_rs16_decode(const Rs16DecArgs &a, hipStream_t s) {
-    if (a.elems == 0 || a.nmiss == 0) return hipSuccess;
+hipError_t launch_rs16_decode(const Rs16DecArgs &a, uint32_t segments, hipStream_t s) {
+    if (a.elems == 0 || a.nmiss == 0 || segments == 0) return hipSuccess;
+    if ((uint64_t)segments * (a.k + a.nmiss) > kRs16DecPtrs || segments > 65535) return hipErrorInvalidValue;
     const size_t tab = (size_t)a.nmiss * a.k * 128u, lds = tab <= rs16k::kRs16DecLds ? tab : 0;
     if (a.k > kRs16MaxK || a.nmiss > kRs16MaxK) return hipErrorInvalidValue;
     // 512-thread blocks: the tables (<= 48 KB) are staged once per 8 waves, not per 2; k <= 32:
     // two elements per thread (elems is a multiple of 32: 64-byte shard blocks)
     if (a.k <= 32 && a.elems % 2) return hipErrorInvalidValue;
     const uint64_t threads = a.k <= 32 ? a.elems / 2 : a.elems;
-    const dim3 grid((uint32_t)((threads + 511) / 512)), block(512);
+    const dim3 grid((uint32_t)((threads + 511) / 512), segments), block(512);
     return rs16k::launch_dec_kb<4>(a, grid, block, lds, s);
 }
 

@@ -97,5 +97,20 @@ def decode_device(k: int, n: int, chunks: list, chunk_bytes: int, d_out, stream=
     _check(r, "decode")
 
 
-__all__ = ["OuterCoder", "ReedSolomonCoder", "encode_device", "decode_device", "MAX_CHUNK_BYTES", "EncodeError",
+def decode_device_batch(k: int, n: int, chunks: list, chunk_bytes: int, d_out, seg_out: int, stream=None) -> None:
+    """te_outer_decode_device_batch: `len(chunks)` segments in one call; chunks[g] is segment g's
+    list of n device chunks (address, tensor or None), its k data chunks go to d_out + g * seg_out.
+    Enqueued on the stream (segments sharing an erasure pattern share launches)."""
+    segs = len(chunks)
+    flat = [None if c is None else (c.data_ptr() if hasattr(c, "data_ptr") else int(c)) for seg in chunks for c in seg]
+    if any(len(seg) != n for seg in chunks):
+        raise ValueError("every segment needs n chunk entries")
+    ptrs = (C.c_void_p * max(1, len(flat)))(*flat)
+    sp = stream.cuda_stream if stream is not None else None
+    r = lib.te_outer_decode_device_batch(k, n, C.cast(ptrs, C.POINTER(C.c_void_p)), segs, chunk_bytes,
+                                         C.c_void_p(d_out.data_ptr()), seg_out, C.c_void_p(sp) if sp else None)
+    _check(r, "decode")
+
+
+__all__ = ["OuterCoder", "ReedSolomonCoder", "encode_device", "decode_device", "decode_device_batch", "MAX_CHUNK_BYTES", "EncodeError",
            "DecodeError", "_lib"]

@@ -137,3 +137,42 @@ def test_decode_device_matches_original(k, n, present):
     d_out = torch.empty(k * cb, dtype=torch.uint8, device="cuda")
     outer.decode_device(k, n, dev, cb, d_out)
     assert d_out.cpu().numpy().tobytes() == b"".join(chunks[:k])
+
+
+def test_decode_device_batch_mixed_patterns():
+    """te_outer_decode_device_batch: 12 segments of OuterCoder(17, 50) in one call, with three
+    erasure patterns among them (parity only, mixed, data only) and more segments per pattern than
+    one launch's shard pointers hold -- every segment's data chunks equal its original bytes, and
+    the per-segment entry point gives the same bytes."""
+    import torch
+    from tape_amd import outer
+    k, n = 17, 50
+    rng = np.random.default_rng(99)
+    segs, keeps, datas = [], [], []
+    for g in range(12):
+        data = rng.bytes(k * 64 * 300 - 5 * g)
+        datas.append(data)
+        chunks = OuterCoder(k, n).encode(data)
+        cb = len(chunks[0])
+        if g % 3 == 0:
+            keep = list(range(k, 2 * k))
+        elif g % 3 == 1:
+            keep = sorted(random.Random(7).sample(range(n), k))
+        else:
+            keep = list(range(k))
+        keeps.append(keep)
+        segs.append([torch.tensor(np.frombuffer(c, np.uint8), device="cuda") if i in keep else None
+                     for i, c in enumerate(chunks)])
+    cb = segs[0][keeps[0][0]].numel()
+    assert all(s[kp[0]].numel() == cb for s, kp in zip(segs, keeps))
+    d_out = torch.zeros(12 * k * cb, dtype=torch.uint8, device="cuda")
+    outer.decode_device_batch(k, n, segs, cb, d_out, k * cb)
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().tobytes()
+    for g in range(12):
+        want = b"".join(OuterCoder(k, n).encode(datas[g])[:k])
+        assert got[g * k * cb:(g + 1) * k * cb] == want, g
+        one = torch.zeros(k * cb, dtype=torch.uint8, device="cuda")
+        outer.decode_device(k, n, segs[g], cb, one)
+        torch.cuda.synchronize()
+        assert one.cpu().numpy().tobytes() == want, g
