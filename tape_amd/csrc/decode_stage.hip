@@ -42,6 +42,9 @@ namespace dstage {
 #ifndef TEC_DEC_MAXG
 #define TEC_DEC_MAXG 2  // waves per workgroup at most (direct output: 2 measured best, 6 -> 2: 7.48 -> 5.95 ms)
 #endif
+#ifndef TEC_DEC_LATE_LD
+#define TEC_DEC_LATE_LD 0  // 1: a step's loads for the next step issued after its own are consumed
+#endif
 #ifndef TEC_DEC_TAB_LDS
 #define TEC_DEC_TAB_LDS 0  // 1: v_perm tables staged in LDS (broadcast reads; r04 A/B: random 5.52 vs 5.51 ms, recover 4.12 vs 3.93); 0: scalar-loaded
 #endif
@@ -219,7 +222,7 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
     };
 
     uint32_t own[NK], part[NK], tkp[NE];
-    auto load_step = [&](uint32_t x) {
+    auto load_known = [&](uint32_t x) {
         const uint32_t zs = (W(x, kDpHdr) & 0xffu) * sc;
         const uint32_t vin = vec_in(x);
 #pragma unroll
@@ -227,8 +230,15 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
             own[j] = ldraw(kbase[j] + zs);
             part[j] = ldopt(W(vin, kDpKd + j));
         }
+    };
+    auto load_tkp = [&](uint32_t x) {
+        const uint32_t vin = vec_in(x);
 #pragma unroll
         for (int e = 0; e < NE; e++) tkp[e] = ldopt(W(vin, kDpEd + e));
+    };
+    auto load_step = [&](uint32_t x) {
+        load_known(x);
+        load_tkp(x);
     };
     // scratch loads of a step, issued after the previous step's scratch stores (lane-private
     // addresses: program order within the lane is the only ordering needed)
@@ -261,7 +271,7 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
         for (int j = 0; j < NK; j++) cown[j] = rot(own[j]), cpart[j] = rot(part[j]);
 #pragma unroll
         for (int e = 0; e < NE; e++) ctkp[e] = rot(tkp[e]);
-        load_step(w_nxt);  // blank step: every partner load dropped
+        if constexpr (!TEC_DEC_LATE_LD) load_step(w_nxt);  // blank step: every partner load dropped
         if constexpr (TEC_DEC_PRIO) __builtin_amdgcn_s_setprio(TEC_DEC_PRIO);
         // ---- uncouple the known nodes: dropped loads read 0, a non-slot partner reads the zero
         // row, a red node masks the PFT term ----
@@ -286,6 +296,9 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
                 for (int j = 0; j < NK; j++) *lds_at(W(lk, kDpKd + j)) = cown[j];
             }
         }
+        // TEC_DEC_LATE_LD: the next step's known-row loads once this step's are consumed (no second
+        // register set for them), its type-1 partner loads after the writes below
+        if constexpr (TEC_DEC_LATE_LD != 0) load_known(w_nxt);
         // pair partners' U (read before this step's writes: a location may be rewritten from its
         // consumer step on)
         uint32_t pu[NE];
@@ -363,6 +376,7 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
                 if (TEC_DEC_DIRECT) put_out(W(oa, kDpEo + e), c0), put_out(W(oc, kDpEo + e), c1);
             }
         }
+        if constexpr (TEC_DEC_LATE_LD != 0) load_tkp(w_nxt);
         load_scr(w_nxt);
         if constexpr (TEC_DEC_PRIO) __builtin_amdgcn_s_setprio(0);
         // the step's rows are staged (and the step before last's flushed); ablation bit 4: timing only
