@@ -43,7 +43,7 @@ namespace dstage {
 #define TEC_DEC_MAXG 2  // waves per workgroup at most (direct output: 2 measured best, 6 -> 2: 7.48 -> 5.95 ms)
 #endif
 #ifndef TEC_DEC_LATE_LD
-#define TEC_DEC_LATE_LD 0  // 1: a step's loads for the next step issued after its own are consumed
+#define TEC_DEC_LATE_LD 1  // 1: a step's loads for the next step issued after its own are consumed (r04: random 5.47 vs 5.52-5.55 ms, recover 3.89 vs 3.94-3.96; 115 VGPRs instead of 127); 0: at the step's start
 #endif
 #ifndef TEC_DEC_TAB_LDS
 #define TEC_DEC_TAB_LDS 0  // 1: v_perm tables staged in LDS (broadcast reads; r04 A/B: random 5.52 vs 5.51 ms, recover 4.12 vs 3.93); 0: scalar-loaded
