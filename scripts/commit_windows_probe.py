@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""te_encode_commit_batch_host on 1024 x 4 MiB pinned objects: GiB/s per hashing group size and
+hashing side (auto / device / host), each size run in several orders, to separate an ordering
+effect from the group size itself (bench.py's copy_inclusive_commit runs 2, 4, 8 GiB in order).
+Prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import tape_amd as T  # noqa: E402
+from tape_amd import batch  # noqa: E402
+
+
+def main():
+    m, L = 1024, 4 << 20
+    s = T.Slicer.clay_default()
+    per = 20 * s.geometry(L).slice_len
+    h_in = torch.randint(0, 256, (m * L,), dtype=torch.uint8).pin_memory()
+    h_out = torch.empty(m * per, dtype=torch.uint8).pin_memory()
+    leaf = torch.empty(m * 20 * 32, dtype=torch.uint8).pin_memory()
+    root = torch.empty(m * 32, dtype=torch.uint8).pin_memory()
+    proof = torch.empty(m * 20 * 5 * 32, dtype=torch.uint8).pin_memory()
+    objs = batch.encode_descs([(i * L, L, i * per, 0) for i in range(m)])
+    res = []
+    for hashing, gib in (("auto", 4), ("auto", 2), ("auto", 4), ("auto", 8), ("auto", 4), ("device", 4),
+                         ("device", 2), ("device", 8), ("host", 4), ("device", 4), ("auto", 4)):
+        batch.set_commit_hashing(hashing)
+        batch.encode_commit_batch_host(s, h_in, objs, h_out, leaf, root, proof, window_bytes=gib << 30)
+        t = time.perf_counter()
+        for _ in range(2):
+            batch.encode_commit_batch_host(s, h_in, objs, h_out, leaf, root, proof, window_bytes=gib << 30)
+        el = time.perf_counter() - t
+        res.append({"hashing": hashing, "group_GiB": gib, "GiBps": round(2 * m * L / el / 2**30, 3)})
+        print(res[-1], flush=True)
+    batch.set_commit_hashing("auto")
+    print(json.dumps({"probe": "encode_commit_batch_host group size / hashing", "runs": res}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
