@@ -1639,8 +1639,15 @@ static int encode_host_impl(te_clay *c, const te_slicer_cfg *cfg, const uint8_t 
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard dg(c->device);
     TE_HIP(dg.err);
-    for (auto &sl : c->pipe)
-        if (!sl.s) TE_HIP(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
+    // three slot streams: the handle's two pipe streams and its own stream -- the same three the
+    // commit pipeline uses (commit_streams).  A third pipe stream made the process's fifth stream
+    // beside the caller's: GPU_MAX_HW_QUEUES is 4, so two streams shared a hardware queue and the
+    // commit path's 30 ms leaf launches blocked copies queued behind them (r04: 4 GiB commit groups
+    // at 7.5 instead of 12.5 GiB/s in a process that had run this path first)
+    if (int r0 = ensure_stream(c)) return r0;
+    for (int k = 0; k < 2; k++)
+        if (!c->pipe[k].s) TE_HIP(hipStreamCreateWithFlags(&c->pipe[k].s, hipStreamNonBlocking));
+    auto slot_stream = [&](size_t k) { return k < 2 ? c->pipe[k].s : c->stream; };
     int rc = TE_OK;
     size_t i = 0, w = 0;
     std::vector<te_object> local;
@@ -1655,18 +1662,19 @@ static int encode_host_impl(te_clay *c, const te_slicer_cfg *cfg, const uint8_t 
             j++;
         }
         te_clay::Slot &sl = c->pipe[w % te_clay::kPipe];
+        const hipStream_t ss = slot_stream(w % te_clay::kPipe);
         if ((rc = hip_status(sl.in.ensure(in_sz + 16))) || (rc = hip_status(sl.out.ensure(out_sz)))) break;
         window_layout(objs, out_bytes, i, j, 0, 0, local, hin, hout);
-        if ((rc = copy_runs(hin, sl.in.as<uint8_t>(), h_data, hipMemcpyHostToDevice, sl.s))) break;
-        rc = encode_enqueue(c, cfg, sl.in.as<uint8_t>(), local.data(), local.size(), sl.out.as<uint8_t>(), sl.s,
+        if ((rc = copy_runs(hin, sl.in.as<uint8_t>(), h_data, hipMemcpyHostToDevice, ss))) break;
+        rc = encode_enqueue(c, cfg, sl.in.as<uint8_t>(), local.data(), local.size(), sl.out.as<uint8_t>(), ss,
                             false, &sl.arena);
         if (rc) break;
-        if ((rc = copy_runs(hout, sl.out.as<uint8_t>(), h_out, hipMemcpyDeviceToHost, sl.s))) break;
+        if ((rc = copy_runs(hout, sl.out.as<uint8_t>(), h_out, hipMemcpyDeviceToHost, ss))) break;
         i = j;
         w++;
     }
-    for (auto &sl : c->pipe) {
-        const int r2 = hip_status(hipStreamSynchronize(sl.s));
+    for (size_t k = 0; k < te_clay::kPipe; k++) {
+        const int r2 = hip_status(hipStreamSynchronize(slot_stream(k)));
         if (rc == TE_OK) rc = r2;
     }
     return rc;
@@ -2270,6 +2278,11 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
         uint64_t max_slice = 0;
         for (size_t o = L.gcut[x]; o < L.gcut[x + 1]; o++) max_slice = std::max<uint64_t>(max_slice, B.slice_len[o]);
         const bool host = host_hash_wins(g_commit_hashing.load(), need_rows * B.n, max_slice, need_out);
+        static const bool trace = tec_knob("TEC_COMMIT_TRACE") != nullptr;  // measurement: the choice per group
+        if (trace)
+            fprintf(stderr, "[tapeec] commit group %zu/%zu: %llu objects, %llu slice bytes, %s hashing (pool %.2f GB/s x %d)\n",
+                    x + 1, ngroups, (unsigned long long)need_rows, (unsigned long long)need_out, host ? "host" : "device",
+                    hh::Pool::get().thread_rate() / 1e9, hh::Pool::get().threads());
         rc = group_open(P, G, need_out, need_rows, row_b);
         if (!rc) rc = group_add(c, cfg, P, G, B, L, x, x + 1 == ngroups && !host, host && pinned_out);
         if (!rc && host) {
