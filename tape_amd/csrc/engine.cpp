@@ -112,8 +112,10 @@ struct DevBuf {
             p = nullptr;
             cap = 0;
         }
+        // large buffers in whole 2 MiB units (the device's large-page size)
         size_t want = std::max<size_t>(n, 4096);
-        want = (want + 4095) & ~(size_t)4095;
+        const size_t unit = want >= ((size_t)64 << 20) ? ((size_t)2 << 20) : 4096;
+        want = (want + unit - 1) & ~(unit - 1);
         hipError_t e = hipMalloc(&p, want);
         if (e != hipSuccess) { p = nullptr; return e; }
         cap = want;
@@ -1640,10 +1642,8 @@ static int encode_host_impl(te_clay *c, const te_slicer_cfg *cfg, const uint8_t 
     DeviceGuard dg(c->device);
     TE_HIP(dg.err);
     // three slot streams: the handle's two pipe streams and its own stream -- the same three the
-    // commit pipeline uses (commit_streams).  A third pipe stream made the process's fifth stream
-    // beside the caller's: GPU_MAX_HW_QUEUES is 4, so two streams shared a hardware queue and the
-    // commit path's 30 ms leaf launches blocked copies queued behind them (r04: 4 GiB commit groups
-    // at 7.5 instead of 12.5 GiB/s in a process that had run this path first)
+    // commit pipeline uses (commit_streams), so with the caller's stream a process holds four
+    // streams for its four hardware queues (GPU_MAX_HW_QUEUES) whichever host paths it runs
     if (int r0 = ensure_stream(c)) return r0;
     for (int k = 0; k < 2; k++)
         if (!c->pipe[k].s) TE_HIP(hipStreamCreateWithFlags(&c->pipe[k].s, hipStreamNonBlocking));
