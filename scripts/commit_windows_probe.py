@@ -40,6 +40,8 @@ def main():
     seq = (("auto", 2), ("auto", 4), ("auto", 8), ("auto", 4)) if pre else \
         (("auto", 4), ("auto", 2), ("auto", 4), ("auto", 8), ("auto", 4), ("device", 4),
          ("device", 2), ("device", 8), ("host", 4), ("device", 4), ("auto", 4))
+    if os.environ.get("SEQ"):  # e.g. SEQ=device:2,auto:4
+        seq = tuple((h, int(g)) for h, g in (x.split(":") for x in os.environ["SEQ"].split(",")))
     for hashing, gib in seq:
         batch.set_commit_hashing(hashing)
         batch.encode_commit_batch_host(s, h_in, objs, h_out, leaf, root, proof, window_bytes=gib << 30)
