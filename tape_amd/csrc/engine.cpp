@@ -2283,13 +2283,21 @@ static int encode_commit_host_impl(te_clay *c, const te_slicer_cfg *cfg, const u
             fprintf(stderr, "[tapeec] commit group %zu/%zu: %llu objects, %llu slice bytes, %s hashing (pool %.2f GB/s x %d)\n",
                     x + 1, ngroups, (unsigned long long)need_rows, (unsigned long long)need_out, host ? "host" : "device",
                     hh::Pool::get().thread_rate() / 1e9, hh::Pool::get().threads());
+        const auto t0 = std::chrono::steady_clock::now();
         rc = group_open(P, G, need_out, need_rows, row_b);
+        const auto t1 = std::chrono::steady_clock::now();
         if (!rc) rc = group_add(c, cfg, P, G, B, L, x, x + 1 == ngroups && !host, host && pinned_out);
+        const auto t2 = std::chrono::steady_clock::now();
         if (!rc && host) {
             jobs.emplace_back();
             rc = group_close_host(P, G, B.n, B.co.height, c->device, jobs.back());
         } else if (!rc) {
             rc = group_close(P, G, B.n, B.co.height, B.leaf_b, B.proof_b);
+        }
+        if (trace) {  // host time enqueueing the group (a long one is a host wait inside)
+            const auto t3 = std::chrono::steady_clock::now();
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            fprintf(stderr, "[tapeec]   host ms: open %.2f add %.2f close %.2f\n", ms(t0, t1), ms(t1, t2), ms(t2, t3));
         }
     }
     for (int k = 0; k < CommitPipe::S; k++) {
