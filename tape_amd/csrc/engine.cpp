@@ -101,17 +101,85 @@ struct DeviceGuard {
     }
 };
 
+// Measurement option (TEC_DEBUG_KNOBS=1 TEC_VMM_BUFS=1): buffers of >= 64 MiB through the virtual
+// memory API -- physical memory created at the recommended granularity and mapped into a fresh
+// address range -- instead of hipMalloc (to test whether a slowdown follows the page placement of
+// re-allocated buffers, DESIGN §4.4's open item).
+static bool vmm_bufs() {
+    static const bool v = [] {
+        const char *s = tec_knob("TEC_VMM_BUFS");
+        return s && s[0] == '1';
+    }();
+    return v;
+}
+
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
+    hipMemGenericAllocationHandle_t vh{};  // VMM allocation (vmm_bufs), else hipMalloc
+    bool vmm = false;
+    hipError_t free_() {
+        if (!p) return hipSuccess;
+        hipError_t e = hipSuccess;
+        if (vmm) {
+            (void)hipDeviceSynchronize();
+            e = hipMemUnmap(p, cap);
+            if (e == hipSuccess) e = hipMemRelease(vh);
+            if (e == hipSuccess) e = hipMemAddressFree(p, cap);
+        } else {
+            e = hipFree(p);
+        }
+        p = nullptr;
+        cap = 0;
+        vmm = false;
+        return e;
+    }
+    hipError_t alloc_vmm(size_t n) {
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        hipMemAllocationProp prop{};
+        prop.type = hipMemAllocationTypePinned;
+        prop.location.type = hipMemLocationTypeDevice;
+        prop.location.id = dev;
+        size_t g = 0;
+        if ((e = hipMemGetAllocationGranularity(&g, &prop, hipMemAllocationGranularityRecommended)) != hipSuccess) return e;
+        if (g == 0) g = (size_t)2 << 20;
+        const size_t sz = (n + g - 1) / g * g;
+        void *va = nullptr;
+        if ((e = hipMemAddressReserve(&va, sz, g, nullptr, 0)) != hipSuccess) return e;
+        hipMemGenericAllocationHandle_t h{};
+        if ((e = hipMemCreate(&h, sz, &prop, 0)) != hipSuccess) {
+            (void)hipMemAddressFree(va, sz);
+            return e;
+        }
+        if ((e = hipMemMap(va, sz, 0, h, 0)) != hipSuccess) {
+            (void)hipMemRelease(h);
+            (void)hipMemAddressFree(va, sz);
+            return e;
+        }
+        hipMemAccessDesc ad{};
+        ad.location = prop.location;
+        ad.flags = hipMemAccessFlagsProtReadWrite;
+        if ((e = hipMemSetAccess(va, sz, &ad, 1)) != hipSuccess) {
+            (void)hipMemUnmap(va, sz);
+            (void)hipMemRelease(h);
+            (void)hipMemAddressFree(va, sz);
+            return e;
+        }
+        p = va;
+        cap = sz;
+        vh = h;
+        vmm = true;
+        return hipSuccess;
+    }
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
         if (p) {
-            hipError_t e = hipFree(p);
+            hipError_t e = free_();
             if (e != hipSuccess) return e;
-            p = nullptr;
-            cap = 0;
         }
+        if (vmm_bufs() && n >= ((size_t)64 << 20)) return alloc_vmm(n);
         // large buffers in whole 2 MiB units (the device's large-page size)
         size_t want = std::max<size_t>(n, 4096);
         const size_t unit = want >= ((size_t)64 << 20) ? ((size_t)2 << 20) : 4096;
@@ -122,11 +190,7 @@ struct DevBuf {
         return hipSuccess;
     }
     template <class T> T *as() const { return reinterpret_cast<T *>(p); }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
+    void release() { (void)free_(); }
 };
 
 struct HostBuf {  // pinned staging for descriptor uploads
