@@ -1,11 +1,12 @@
 #!/bin/bash
-# round-4 GPU call: what bounds the table-driven decode kernel -- random-pattern decode with the
-# shipped build and with ablation builds (varlib/lib_dec_abl*.so: 1 no scratch loads, 2 no MDS
+# what bounds the table-driven decode kernel -- random-pattern decode with the
+# shipped build and with ablation builds (varlib/lib_dec_abl*.so, built first with scripts/build_var.sh
+# dec_ablN "-DTEC_DEC_ABLATE=N" decode_stage.hip: 1 no scratch loads, 2 no MDS
 # products, 8 no input loads, 9 = 1+8, 11 = 1+2+8); outputs of ablations are wrong by design
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r4k
+O=gpurun_out/decode_ablations
 mkdir -p $O
 B="python -u bench.py --steps 10 --warmup 3 --cpu-sample 0 --copy-objects 0 --mode decode --pattern random"
 timeout -k 10 300 $B > $O/base.json 2> $O/base.err || exit 1

@@ -1,8 +1,8 @@
 #!/bin/bash
-# round-4 final GPU call: whole GPU suite (verbose, per-test limit), smoke, default bench line, stream-shape line
+# whole GPU suite (verbose, per-test limit), smoke, and the bench lines: default, stream shape, random decode, recover, outer
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r4z3
+O=gpurun_out/final
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
 tail -5 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc

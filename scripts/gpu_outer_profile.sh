@@ -1,9 +1,9 @@
 #!/bin/bash
-# round-4 GPU call: OuterCoder kernels -- bench line, kernel stats, SQ instruction / wait counters
+# OuterCoder kernels -- bench line, kernel stats, SQ instruction / wait counters
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r4l
+O=gpurun_out/outer_profile
 mkdir -p $O
 B="python3 bench.py --mode outer --steps 3 --warmup 1 --cpu-sample 0"
 timeout -k 10 300 python3 -u bench.py --mode outer --cpu-sample 0 > $O/outer.json 2> $O/outer.err && cat $O/outer.json &&

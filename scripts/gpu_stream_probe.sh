@@ -1,10 +1,10 @@
 #!/bin/bash
-# round-4 GPU call: stream-shape latency probes -- submit-call time, the pool's aggregate hash rate,
+# stream-shape latency probes -- submit-call time, the pool's aggregate hash rate,
 # row-piece size and lane count A/B
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r4g
+O=gpurun_out/stream_probe
 mkdir -p $O
 S="python -u bench.py --mode stream --stream-chunks 64 --cpu-sample 0"
 timeout -k 10 300 $S > $O/stream.json 2> $O/stream.err && cat $O/stream.json &&
