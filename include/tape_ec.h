@@ -446,7 +446,9 @@ int te_outer_decode_device(uint32_t k, uint32_t n, const uint8_t *const *d_chunk
 /* The same for `segments` segments in one call (a snapshot read): segment g's chunk i at
  * d_chunks[g * n + i] (host array of DEVICE pointers, NULL = missing), its k data chunks to
  * d_out + g * seg_out.  Segments sharing an erasure pattern share launches (up to 256 shard
- * pointers each).  Enqueued on hip_stream; returns without waiting. */
+ * pointers each).  seg_out >= k * chunk_bytes when segments > 1 (TE_ERR_INVALID_ARG otherwise).
+ * Every segment is validated before anything is enqueued.  Enqueued on hip_stream; returns
+ * without waiting. */
 int te_outer_decode_device_batch(uint32_t k, uint32_t n, const uint8_t *const *d_chunks, uint32_t segments,
                                  uint64_t chunk_bytes, uint8_t *d_out, uint64_t seg_out, void *hip_stream);
 

@@ -3751,6 +3751,7 @@ int outer_decode_segs(uint32_t k, uint32_t n, const uint8_t *const *d_chunks, ui
     if (k == 0 || k > n || !d_chunks || !d_out || segments == 0) return TE_ERR_INVALID_ARG;
     const uint32_t m = n - k;
     if (chunk_bytes == 0 || chunk_bytes % 64 || chunk_bytes / 2 > 0xffffffffull) return TE_ERR_INVALID_LAYOUT;
+    if (segments > 1 && seg_out < (uint64_t)k * chunk_bytes) return TE_ERR_INVALID_ARG;  // segment outputs would overlap
     // validate every segment before anything is enqueued
     std::map<std::vector<uint32_t>, std::vector<uint32_t>> groups;  // recv | miss -> segments
     for (uint32_t g = 0; g < segments; g++) {

@@ -257,3 +257,27 @@ def test_serve_repair_request_errors(oracle):
             T.serve_repair_request(s.coder, blob, req)
         assert msg in str(e.value), (msg, str(e.value))
     assert T.serve_repair_request(s.coder, sl, []) == b""
+
+
+def test_outer_decode_batch_argument_checks():
+    """te_outer_decode_device_batch validates every segment before enqueueing anything or touching a
+    device: chunk_bytes not a multiple of 64 is INVALID_LAYOUT, overlapping segment outputs are an
+    invalid argument, a segment with fewer than k chunks is NOT_ENOUGH_SLICES (outer.rs:127-129)
+    even when the segments before it are complete, and a valid call without a device is NO_DEVICE."""
+    k, n, cb = 4, 6, 128
+    fake = 1 << 20  # never dereferenced: every path below returns before device work
+
+    def call(segs, chunk_bytes=cb, seg_out=k * cb):
+        flat = [None if x is None else fake + 4096 * i for i, x in enumerate(c for s in segs for c in s)]
+        ptrs = (C.c_void_p * len(flat))(*flat)
+        return _lib.lib.te_outer_decode_device_batch(k, n, C.cast(ptrs, C.POINTER(C.c_void_p)), len(segs),
+                                                     chunk_bytes, C.c_void_p(fake), seg_out, None)
+    full = [1] * n
+    two_missing = [None, 1, None, 1, 1, 1]
+    three_missing = [None, None, None, 1, 1, 1]
+    assert call([full], chunk_bytes=100) == _lib.TE_ERR_INVALID_LAYOUT
+    assert call([full, full], seg_out=k * cb - 64) == _lib.TE_ERR_INVALID_ARG
+    assert call([full, two_missing, three_missing]) == _lib.TE_ERR_NOT_ENOUGH_SLICES
+    if _lib.device_count() == 0:
+        assert call([full, two_missing, two_missing]) == _lib.TE_ERR_NO_DEVICE
+        assert call([full], seg_out=0) == _lib.TE_ERR_NO_DEVICE  # one segment: seg_out unused
