@@ -140,9 +140,132 @@ def gpu_env(torch, dev) -> dict:
     return out
 
 
+def box_ceiling(torch, d_in, in_bytes, d_out, out_bytes, stream, alg_bytes) -> dict | None:
+    """This box's HBM ceiling for the encode's byte mix (tape_amd/csrc/hbm_probe.hip, measurement
+    only): the step's object bytes read once and slice bytes written once by a compute-free,
+    barrier-free streaming kernel on the bench's own buffers, before the timed region.  "blocks":
+    contiguous 1 KiB wave-blocks (the best any encode kernel could do); "rows": the output as the
+    slices' 1,430-byte sub-chunk rows (what the row shape alone costs).  GB/s = alg bytes / ms."""
+    import ctypes as C
+    try:
+        lib = C.CDLL(os.path.join(ROOT, "tape_amd", "libtecprobe.so"))
+    except OSError as e:
+        return {"error": str(e)[:100]}
+    f = lib.tec_probe_encode_mix
+    f.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                  C.POINTER(C.c_float)]
+    res = {}
+    for name, shape, wgs in (("blocks", 0, 1024), ("blocks", 0, 2048), ("rows", 1, 1024)):
+        ms = C.c_float()
+        r = f(d_in.data_ptr(), in_bytes, d_out.data_ptr(), out_bytes, shape, wgs, 5, C.c_void_p(stream.cuda_stream),
+              C.byref(ms))
+        if r:
+            return {"error": f"probe failed ({r})"}
+        key = f"{name}_ms"
+        res[key] = min(res.get(key, 1e9), round(ms.value, 4))
+    torch.cuda.synchronize()
+    return {"blocks_ms": res["blocks_ms"], "rows_ms": res["rows_ms"],
+            "blocks_GBps": round(alg_bytes / res["blocks_ms"] / 1e6, 1),
+            "rows_GBps": round(alg_bytes / res["rows_ms"] / 1e6, 1),
+            "blocks_frac_of_peak": round(alg_bytes / res["blocks_ms"] / 1e6 / PEAK_HBM_GBS, 4)}
+
+
+def dev_of(torch, world: int, local: int):
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+    return dev
+
+
 def rank_objects(rank: int, nobj: int) -> tuple[int, int]:
     """Contiguous global object range [first, first + nobj) of this rank (weak scaling)."""
     return rank * nobj, rank * nobj + nobj
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """`--gpus N` (N > 1) without an external launcher: start N worker processes of this same
+    script, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in their
+    environment (what torch.distributed.run would set), then wait for all of them.  This process
+    never touches the GPU (no torch.cuda call, no libtapeec load) and never re-execs: the workers
+    are children.  Rank 0 prints the one JSON line; if any rank fails, the others are stopped (by
+    their own PIDs) and the first failing exit code is returned.  The reference's equivalent
+    concurrency is the stream writer's worker pool (sdk/src/stream/write.rs:54-57, 329-362)."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TEC_BENCH_LAUNCHED="1")
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"[bench] rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in pending:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
+def launcher_check(args) -> None:
+    """`--launcher-check` (CPU, gloo; tests/test_bench_launcher.py): the multi-rank plumbing of a
+    bench run without a GPU -- process group, rank partition of the object ids, each rank's
+    SplitMix64 objects, the max-over-ranks time -- gathered to rank 0, which prints one JSON line
+    with the digests of every rank's objects (the test checks them against the oracle)."""
+    import hashlib
+    import torch
+    import torch.distributed as dist
+    world, rank, _ = dist_setup(torch, dist, "gloo")
+    share, batch_objs = rank_share(args, world)
+    first, end = rank_objects(rank, share)
+    L = args.object_bytes
+    buf = torch.empty(share * L, dtype=torch.uint8)
+    splitmix_fill(torch, buf, first, share, L)
+    digests = [hashlib.sha256(buf[i * L:(i + 1) * L].numpy().tobytes()).hexdigest() for i in range(share)]
+    t = max_over_ranks(torch, dist, world, 1.0 + rank, torch.device("cpu"))
+    got = [None] * world
+    if world > 1:
+        dist.all_gather_object(got, {"rank": rank, "first": first, "end": end, "digests": digests,
+                                     "pid": os.getpid()})
+    else:
+        got = [{"rank": 0, "first": first, "end": end, "digests": digests, "pid": os.getpid()}]
+    if rank == 0:
+        print(json.dumps({"metric": "launcher check (no GPU)", "n_gpus": world,
+                          "world_size": dist.get_world_size() if world > 1 else 1,
+                          "backend": dist.get_backend() if world > 1 else None,
+                          "objects_per_gpu": share, "device_batch_objects": batch_objs,
+                          "total_objects": share * world, "max_over_ranks_s": t, "ranks": got}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+CONFIG5_TOTAL_OBJECTS = 16_384  # BASELINE.json configs[4]: 64 GiB stream of 4 MiB objects over 8 GPUs
+CONFIG5_DEVICE_BATCH = 2_048    # one GPU's share at N = 8 (SURVEY 8d config 5)
+
+
+def rank_share(args, world: int) -> tuple[int, int]:
+    """(objects this rank encodes per step, objects per device batch).  Default: --objects per GPU
+    (weak scaling).  --workload config5: the 64 GiB stream of 16,384 objects split over the ranks
+    (2,048 per GPU at N = 8; strong scaling), encoded in device batches of <= 2,048 objects."""
+    if args.workload == "config5":
+        if CONFIG5_TOTAL_OBJECTS % world:
+            raise SystemExit(f"--workload config5 needs a world size dividing {CONFIG5_TOTAL_OBJECTS}")
+        share = CONFIG5_TOTAL_OBJECTS // world
+        return share, min(share, CONFIG5_DEVICE_BATCH)
+    return args.objects, args.objects
 
 
 def max_over_ranks(torch, dist, world: int, seconds: float, dev) -> float:
@@ -190,7 +313,26 @@ def main():
                     help="--mode repair: 1 = slice (lost + 10) mod 20 is down too, so every stripe's "
                          "helper set skips one node of the other column (a peer outage)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--workload", choices=["default", "config5"], default="default",
+                    help="encode mode: default = --objects per GPU (config 2, weak scaling); config5 = the "
+                         "64 GiB stream of 16,384 x 4 MiB objects split over the N ranks (2,048 per GPU at "
+                         "N = 8), device batches of <= 2,048, plus a copy-inclusive leg per rank")
+    ap.add_argument("--sdk-chunks", type=int, default=16,
+                    help="encode mode: chunks in the short SDK-shape stream leg (64 MiB chunks, 4 in flight, "
+                         "pinned, the library's hashing choice; 0 = skip)")
+    ap.add_argument("--launcher-check", action="store_true",
+                    help="CPU only (gloo): run the multi-rank plumbing without a GPU (tests)")
     args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and env_world is None:
+        # no external launcher: one worker process per GPU, started before anything here touches
+        # the GPU (this process never initialises HIP)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus and not os.environ.get("TEC_BENCH_LAUNCHED"):
+        print(f"[bench] WORLD_SIZE={env_world} from the launcher overrides --gpus {args.gpus}", file=sys.stderr)
+    if args.launcher_check:
+        return launcher_check(args)
 
     import numpy as np
     import torch
@@ -199,8 +341,11 @@ def main():
     from tape_amd import batch
 
     world, rank, local = dist_setup(torch, dist, "nccl")
-    dev = torch.device("cuda", local if world > 1 else 0)
-    torch.cuda.set_device(dev)
+    if args.workload == "config5":
+        if args.mode != "encode":
+            raise SystemExit("--workload config5 is an encode workload")
+        return config5_bench(args, torch, dist, world, rank, dev_of(torch, world, local), np, T, batch)
+    dev = dev_of(torch, world, local)
     T.lib.te_set_device(dev.index)
 
     if args.mode == "outer":
@@ -288,6 +433,9 @@ def main():
         def step():
             merkle.commit_batch(d_out, per, g.slice_len, N, nobj, d_leaf, d_root, d_proof, T.SLICE_TREE_HEIGHT, stream)
 
+    ceiling = None
+    if args.mode == "encode" and unit_bytes:  # this box's HBM on the encode's exact byte mix, same buffers
+        ceiling = box_ceiling(torch, d_in, nobj * L, d_out, nobj * per, stream, unit_bytes * nobj)
     if args.mode in ("decode", "recover") and args.decode_jit == "off":
         slicer.coder.set_decode_jit("off")
     # (recover: 20 patterns x ~64 stripes per window -- below the engine's 512-stripe floor for a
@@ -374,11 +522,25 @@ def main():
         copy_inc = copy_inclusive(args, torch, dist, world, slicer, batch, d_in, d_out, per, L, dev)
         copy_commit = copy_inclusive_commit(args, torch, dist, world, slicer, batch, d_in, d_out, per, L, dev)
 
+    sdk_stream = None
+    if args.mode == "encode" and args.copy_objects != 0 and args.sdk_chunks > 0:
+        sdk_stream = stream_sdk_short(args, torch, dist, world, rank, dev, T, batch)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0 and args.mode == "encode":  # rank 0 at N=1 only
         cpu = cpu_baseline(args, np, torch, d_in, d_out, per, L)
     if rank == 0 and world == 1 and args.cpu_sample > 0 and args.mode == "commit":
         cpu = cpu_baseline_commit(args, d_out, per, g.slice_len, L)
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and args.mode in ("decode", "repair", "recover"):
+        if args.mode == "decode":
+            cpu = cpu_baseline_mode(args, np, "decode", d_out, per, g.slice_len, L, d_dec, L, masks=masks)
+        elif args.mode == "repair":
+            lost = [i % N for i in range(nobj)]
+            down = [(l + 10) % N if args.unavailable else -1 for l in lost]
+            cpu = cpu_baseline_mode(args, np, "repair", d_out, per, g.slice_len, L, d_rep, g.slice_len,
+                                    lost=lost, down=down)
+        else:
+            cpu = cpu_baseline_mode(args, np, "recover", d_out, per, g.slice_len, L, d_rec, g.slice_len,
+                                    masks=[o[2] for o in rec_objs], lost=[o[3] for o in rec_objs])
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -396,6 +558,7 @@ def main():
             "value": round(gib_s, 3),
             "unit": "GiB/s",
             "n_gpus": world,
+            **comm_info(dist, world),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -418,11 +581,15 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4) if achieved else None,
                          "traffic": traffic,
                          "alg_bytes_per_launch": unit_bytes * nobj if unit_bytes else None,
-                         "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
+                         "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                         "box_ceiling": ceiling,
+                         "box_ceiling_frac": round(achieved / ceiling["blocks_GBps"], 4)
+                         if ceiling and achieved else None},
             "cpu_baseline": cpu,
             "gpu": gpu_env(torch, dev),
             "copy_inclusive": copy_inc,
             "copy_inclusive_encode_commit": copy_commit,
+            "stream_sdk_shape": sdk_stream,
             "commit_GiBps_vs_objects": commit_sweep,
             "outputs_verified": verified,
         }
@@ -431,6 +598,137 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def config5_bench(args, torch, dist, world, rank, dev, np, T, batch):
+    """--workload config5 (BASELINE.json configs[4]): the 64 GiB synthetic write
+    stream chunked at 4 MiB -- 16,384 objects -- encode partitioned across the N ranks, each rank its
+    contiguous range of 16,384 / N objects (2,048 at N = 8) with no data-path collective.  The
+    rank's objects are resident in HBM (64 GiB at N = 1); one step encodes all of them in device
+    batches of <= 2,048 objects into one 2,048-object slice buffer.  `value` = 64 GiB / the step time
+    (max over ranks): the whole job, so `scaling` is "strong".  Then a copy-inclusive leg per rank:
+    the rank's objects from pinned host memory to pinned host slices through te_encode_batch_host
+    over a host ring of <= 1,024 objects (4 GiB in, 14.6 GB out), every rank at once."""
+    L = args.object_bytes
+    share, nb = rank_share(args, world)
+    first, _ = rank_objects(rank, share)
+    slicer = T.Slicer.clay_default()
+    g = slicer.geometry(L)
+    per = N * g.slice_len
+    d_in = torch.empty(share * L, dtype=torch.uint8, device=dev)
+    splitmix_fill(torch, d_in, first, share, L)
+    d_out = torch.empty(nb * per, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    descs = batch.encode_descs([(i * L, L, i * per, 0) for i in range(nb)])
+    views = [d_in[b * nb * L:(b + 1) * nb * L] for b in range(share // nb)]
+
+    def step():
+        for v in views:
+            batch.encode_batch(slicer, v, descs, d_out, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    batch.kernel_time_ms()
+    batch.kernel_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    mine = time.perf_counter() - t0
+    batch.kernel_timing(False)
+    kms, _ = batch.kernel_time_ms()
+    per_rank = gather_floats(torch, dist, world, mine, dev)
+    elapsed = max(per_rank)
+    total = share * world
+    avg_launch_s = kms / max(1, args.steps * len(views)) / 1e3
+    achieved = ALG_BYTES["encode"] * nb / avg_launch_s / 1e9 if L == 4 * MiB else None
+    # the timed outputs of the last batch: decode(slices 13..19) == the objects, on every rank
+    metas = b"".join(d_out[i * per + g.slice_len - 48:i * per + g.slice_len].cpu().numpy().tobytes() for i in range(nb))
+    dec_objs = batch.decode_descs([(i * per, g.slice_len, sum(1 << j for j in range(13, 20)), i * L) for i in range(nb)])
+    d_dec = torch.empty(nb * L, dtype=torch.uint8, device=dev)
+    slicer.coder.set_decode_jit("off")
+    batch.decode_batch(slicer, d_out, dec_objs, metas, d_dec, stream)
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(d_dec, views[-1]))
+    del d_dec
+    oks = gather_floats(torch, dist, world, 1.0 if ok else 0.0, dev)
+    # copy-inclusive: pinned host -> host over a ring of <= 1,024 objects, the rank's share streamed through it
+    ring = min(share, 1024)
+    h_in = torch.empty(ring * L, dtype=torch.uint8).pin_memory()
+    h_in.copy_(d_in[:ring * L])
+    h_out = torch.empty(ring * per, dtype=torch.uint8).pin_memory()
+    hobjs = batch.encode_descs([(i * L, L, i * per, 0) for i in range(ring)])
+    batch.encode_batch_host(slicer, h_in, hobjs, h_out)  # warm-up (pipeline buffers)
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter()
+    for _ in range(share // ring):
+        batch.encode_batch_host(slicer, h_in, hobjs, h_out)
+    cmine = time.perf_counter() - t
+    c_rank = gather_floats(torch, dist, world, cmine, dev)
+    # the ring's first and last object against a device-resident encode of the same bytes
+    batch.encode_batch(slicer, d_in, descs, d_out, stream)
+    torch.cuda.synchronize()
+    cok = bool(torch.equal(h_out[:per], d_out[:per].cpu()) and
+               torch.equal(h_out[(ring - 1) * per:ring * per], d_out[(ring - 1) * per:ring * per].cpu()))
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        import argparse as _ap
+        a2 = _ap.Namespace(**vars(args))
+        a2.objects = nb
+        cpu = cpu_baseline(a2, np, torch, d_in, d_out, per, L)  # d_out now holds the first batch's slices
+    if rank == 0:
+        print(json.dumps({
+            "metric": "device-resident encode GiB/s, 64 GiB stream of 4 MiB objects partitioned over the GPUs "
+                      "(BASELINE config 5)",
+            "value": round(total * L / elapsed / 2**30, 3), "unit": "GiB/s", "n_gpus": world,
+            **comm_info(dist, world),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (SplitMix64 per object, seed 0x7A9E5EED ^ id), device-resident",
+            "config": {"workload": f"Slicer::encode of the 64 GiB stream ({total} x {L} B objects), {share} contiguous "
+                                   f"objects per GPU in device batches of {nb}, Clay(20,7,16) rotated, 1 MB stripes",
+                       "total_objects": total, "objects_per_gpu": share, "device_batch_objects": nb,
+                       "object_bytes": L, "profile": "clay(20,7,16)",
+                       "parallelism": f"objects partitioned over {world} GPU(s), no collective"},
+            "rank_ms_per_step": [round(x * 1e3 / args.steps, 3) for x in per_rank],
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4) if achieved else None,
+                         "traffic": None, "alg_bytes_per_launch": ALG_BYTES["encode"] * nb,
+                         "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
+            "cpu_baseline": cpu, "gpu": gpu_env(torch, dev),
+            "copy_inclusive": {"value": round(total * L / max(c_rank) / 2**30, 3), "unit": "GiB/s", "pinned": True,
+                               "host_ring_objects": ring, "rank_ms": [round(x * 1e3, 1) for x in c_rank],
+                               "note": "each rank's share streamed from a pinned host ring of the first `host_ring_objects` "
+                                       "objects through te_encode_batch_host, all ranks at once (node PCIe and host "
+                                       "memory shared)", "matches_device_resident": cok},
+            "outputs_verified": all(x == 1.0 for x in oks)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def gather_floats(torch, dist, world: int, x: float, dev) -> list:
+    """Every rank's value of x (all_gather over the process group; only timings and flags travel)."""
+    if world <= 1:
+        return [x]
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [float(o.item()) for o in out]
+
+
+def comm_info(dist, world: int) -> dict:
+    """The process group as the collective library saw it (RCCL is torch's "nccl" backend on ROCm)."""
+    if world <= 1 or not dist.is_initialized():
+        return {"world_size": 1, "backend": None}
+    return {"world_size": dist.get_world_size(), "backend": str(dist.get_backend())}
 
 
 def outer_bench(args, torch, dist, world, rank, dev):
@@ -687,6 +985,98 @@ def stream_bench(args, torch, dist, world, rank, dev):
         dist.destroy_process_group()
 
 
+def stream_sdk_short(args, torch, dist, world, rank, dev, T, batch) -> dict:
+    """The SDK's stream-write shape as a short leg of the default encode line: a
+    stream of `--sdk-chunks` x 64 MiB chunks (MAX_TRACK_SIZE, sdk/src/stream/manifest.rs:22), one
+    encode_with_proofs window per chunk through te_stream_writer, at most 4 in flight
+    (MAX_ENCODE_WORKERS, sdk/src/stream/write.rs:54-57, 332-362), pinned host buffers in a ring of
+    8 slots, the library's hashing choice (host cores for these 9.7 MB slices).  Copy-inclusive:
+    chunk bytes in host memory, slices + leaf hashes + roots + proofs back in host memory.  The last
+    chunk is checked against a device-resident encode and hashlib; the CPU figure is the oracle's
+    encode + hashlib of 4 chunks on 4 threads (the SDK's own worker count)."""
+    import collections
+    import hashlib
+    CB, nch, depth, H = 64 * MiB, args.sdk_chunks, 4, T.SLICE_TREE_HEIGHT
+    s = T.Slicer.clay_default()
+    g = s.geometry(CB)
+    per = N * g.slice_len
+    R = 2 * depth
+    first, _ = rank_objects(rank, nch)
+    d_src = torch.empty(R * CB, dtype=torch.uint8, device=dev)
+    splitmix_fill(torch, d_src, first, R, CB)
+    pin = lambda n: torch.empty(n, dtype=torch.uint8).pin_memory()
+    r = {"in": [pin(CB) for _ in range(R)], "out": [pin(per) for _ in range(R)],
+         "leaf": [pin(N * 32) for _ in range(R)], "root": [pin(32) for _ in range(R)],
+         "proof": [pin(N * H * 32) for _ in range(R)]}
+    for k in range(R):
+        r["in"][k].copy_(d_src[k * CB:(k + 1) * CB])
+    descs = [batch.encode_descs([(0, CB, 0, first + c)]) for c in range(nch)]
+    sw = batch.StreamWriter([s], height=H, hashing="auto")
+    lat = []
+
+    def run(chunks):
+        inflight, t_sub = collections.deque(), {}
+        del lat[:]
+        for c in range(chunks):
+            k = c % R
+            if len(inflight) >= depth:
+                t = inflight.popleft()
+                sw.wait(t)
+                lat.append(time.perf_counter() - t_sub.pop(t))
+            t_sub_c = time.perf_counter()
+            t = sw.submit(r["in"][k], descs[c], r["out"][k], r["leaf"][k], r["root"][k], r["proof"][k])
+            t_sub[t] = t_sub_c
+            inflight.append(t)
+        while inflight:
+            t = inflight.popleft()
+            sw.wait(t)
+            lat.append(time.perf_counter() - t_sub.pop(t))
+
+    run(min(nch, R))  # warm-up: buffers, hashing pool
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    run(nch)
+    el = max_over_ranks(torch, dist, world, time.perf_counter() - t0, dev)
+    sw.close()
+    k = (nch - 1) % R
+    d_out = torch.empty(per, dtype=torch.uint8, device=dev)
+    batch.encode_batch(s, d_src[k * CB:(k + 1) * CB], [(0, CB, 0, first + nch - 1)], d_out)
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(r["out"][k], d_out.cpu()))
+    sl = r["out"][k].numpy()
+    lv = r["leaf"][k].numpy().tobytes()
+    for j in range(N):
+        h = hashlib.sha256(b"LEAF")
+        h.update(memoryview(sl[j * g.slice_len:(j + 1) * g.slice_len]))
+        ok = ok and lv[j * 32:(j + 1) * 32] == h.digest()
+    ls = sorted(lat)
+    out = {"value": round(nch * world * CB / el / 2**30, 3), "unit": "GiB/s", "chunks_per_gpu": nch,
+           "chunk_bytes": CB, "in_flight": depth, "pinned": True, "hashing": "auto (host cores for 64 MiB chunks)",
+           "ms_per_chunk": round(el / nch * 1e3, 2),
+           "chunk_latency_ms_p50_p90": [round(ls[len(ls) // 2] * 1e3, 2), round(ls[(9 * len(ls)) // 10] * 1e3, 2)],
+           "host_hash_threads": batch.host_hash_threads(), "outputs_verified": ok, "cpu_baseline": None}
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        from concurrent.futures import ThreadPoolExecutor
+        from oracle import oracle as O
+        from oracle import merkle_oracle as MO
+        clay = O.OracleClay(20, 7, 16)
+
+        def one(kk):
+            slc = O.slicer_encode_np(clay, r["in"][kk].numpy(), chunk_index=first + kk)
+            leaves = [hashlib.sha256(b"LEAF" + slc[j].tobytes()).digest() for j in range(N)]
+            return MO.root_from_leaf_hashes(leaves, H)
+        t = time.perf_counter()
+        with ThreadPoolExecutor(4) as ex:
+            list(ex.map(one, range(4)))
+        out["cpu_baseline"] = {"value": round(4 * CB / (time.perf_counter() - t) / 2**30, 3), "unit": "GiB/s",
+                               "cores": 4, "kind": "port",
+                               "sample": "4 x 64 MiB chunks on 4 threads (the SDK's MAX_ENCODE_WORKERS): oracle "
+                                         "Slicer::encode + hashlib SHA-256 leaves + merkle root"}
+    del d_src, r
+    return out
+
+
 def percall_bench(args, torch, dist, world, rank, dev):
     """--mode percall: the unchanged callers' shape.  lib/slicer's callers use one
     object per call with pageable Vec<u8>s: Slicer::encode per track (sdk/src/track/write.rs:273-308,
@@ -825,6 +1215,39 @@ def cpu_baseline_stream(args, r, CB, R, first=0):
                       "+ hashlib SHA-256 leaves + merkle root and proofs",
             "sdk_4_workers_GiBps": round(res[4], 3), "single_thread_GiBps": round(res[1], 3),
             "affinity_cores": cores, "root_matches_gpu": bool(ok)}
+
+
+def cpu_baseline_mode(args, np, mode, d_out, per, slice_len, L, d_gpu, out_stride, masks=None, lost=None, down=None):
+    """CPU baseline of the decode / repair / recover lines (the oracle, kind "port": the reference's
+    Rust crate cannot run here): the same objects and the same survivor / lost / down choices as the
+    GPU step, one object per thread on the GPU's host share (16 threads), then the same entry point
+    on one thread over 16 objects; the oracle's outputs are byte-compared with the GPU's timed
+    outputs of the sample.  Rate in GiB/s of objects, as `value`."""
+    from oracle import oracle as O
+    cores = len(os.sched_getaffinity(0))
+    thr = args.cpu_threads or max(1, min(16, cores))
+    m = min(args.cpu_sample, args.objects)
+    host = d_out[:m * per].cpu().numpy()
+    clay = O.OracleClay(20, 7, 16)
+    out = np.zeros(m * out_stride, np.uint8)
+    sel = lambda v, k: None if v is None else list(v)[:k]
+    t = time.perf_counter()
+    bad = O.slicer_many(clay, mode, host, per, slice_len, m, out, out_stride, thr, sel(masks, m), sel(lost, m),
+                        sel(down, m))
+    wall = time.perf_counter() - t
+    match = bad == 0 and bool(np.array_equal(d_gpu[:m * out_stride].cpu().numpy(), out))
+    m1 = min(m, 16)
+    t = time.perf_counter()
+    O.slicer_many(clay, mode, host, per, slice_len, m1, out, out_stride, 1, sel(masks, m1), sel(lost, m1), sel(down, m1))
+    single = m1 * L / (time.perf_counter() - t) / 2**30
+    what = {"decode": "Slicer::decode from the same 7 slices per object",
+            "repair": "plan + helper sub-chunk gather + Slicer::repair of the same lost slice per object",
+            "recover": "Slicer::decode from the same 7 slices + Slicer::encode, keep the lost slice (recover.rs:411-442)"}
+    return {"value": round(m * L / wall / 2**30, 4), "unit": "GiB/s", "cores": thr, "kind": "port",
+            "sample": f"{m} x 4 MiB objects (first {m} of the batch), {thr} threads, one object per thread: oracle "
+                      f"{what[mode]} (oracle/clay_oracle.c oc_slicer_many)",
+            "single_thread_GiBps": round(single, 4), "single_thread_objects": m1, "affinity_cores": cores,
+            "gpu_matches_oracle_on_sample": match}
 
 
 def cpu_baseline_commit(args, d_out, per, slice_len, L):

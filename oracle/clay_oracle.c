@@ -703,3 +703,113 @@ int oc_slicer_encode_many(const oc_clay *c, const uint8_t *data, size_t len, int
     for (int i = 0; i < nthr; i++) pthread_join(th[i], NULL);
     return 0;
 }
+
+/* ---------------- CPU baseline helpers for the decode / repair / recover bench lines ----------------
+ * One object per task, tasks spread over nthr threads (the same shape as oc_slicer_encode_many).
+ * Object o's 20 slices are at slices + o * obj_stride (slice i at + i * slice_len). */
+typedef struct {
+    const oc_clay *c; const uint8_t *slices; size_t obj_stride, slice_len; const uint32_t *masks;
+    const int *lost; const int *down; uint8_t *out; size_t out_stride; int nobj, tid, nthr, kind; int *status;
+} many_job;
+
+/* Slicer::decode from the slices marked in masks[o] (slicer.rs:298-364) */
+static int decode_one(const many_job *j, int o) {
+    int av[OC_MAXQT];
+    for (int i = 0; i < j->c->n; i++) av[i] = (j->masks[o] >> i) & 1;
+    long r = oc_slicer_decode(j->c, 1, j->slices + (size_t)o * j->obj_stride, av, j->slice_len,
+                              j->out + (size_t)o * j->out_stride);
+    return r < 0 ? (int)r : 0;
+}
+
+/* Slicer::repair of slice lost[o] (repair.rs:324-367): plan from the available slices (all but
+ * lost[o] and down[o]), the helpers' sub-chunks gathered per stripe as extract_repair_data sends
+ * them (repair.rs:97-130), ClayCode::repair per stripe, then the metadata suffix. */
+static int repair_one(const many_job *j, int o) {
+    const oc_clay *c = j->c;
+    int n = c->n, d = c->d, beta = c->beta, lost = j->lost[o], down = j->down ? j->down[o] : -1;
+    const uint8_t *base = j->slices + (size_t)o * j->obj_stride;
+    const uint8_t *meta = base + j->slice_len - OC_META;
+    uint64_t blob_len = get_u64(meta + 8), S = get_u64(meta + 16);
+    int avail[OC_MAXQT], na = 0;
+    for (int i = 0; i < n; i++) if (i != lost && i != down) avail[na++] = i;
+    size_t ns = oc_num_stripes(blob_len, S);
+    int *ls = (int *)malloc(sizeof(int) * ns), *hsl = (int *)malloc(sizeof(int) * ns * d);
+    int *hsh = (int *)malloc(sizeof(int) * ns * d), *pl = (int *)malloc(sizeof(int) * ns * d * beta);
+    long cs = oc_repair_plan(c, 1, lost, avail, na, blob_len, S, ls, hsl, hsh, pl);
+    int rc = 0;
+    if (cs <= 0) { rc = -1; goto done; }
+    size_t sc = (size_t)cs / c->alpha, rb = (size_t)beta * sc;
+    uint8_t *hb = (uint8_t *)malloc((size_t)d * rb);
+    uint8_t *dst = j->out + (size_t)o * j->out_stride;
+    for (size_t s = 0; s < ns && !rc; s++) {
+        int ids[OC_MAXQT], ord[OC_MAXQT];
+        for (int h = 0; h < d; h++) ord[h] = h;
+        for (int a = 0; a < d; a++)       /* oc_clay_repair takes helpers by ascending shard id */
+            for (int b = a + 1; b < d; b++)
+                if (hsh[s * d + ord[b]] < hsh[s * d + ord[a]]) { int t = ord[a]; ord[a] = ord[b]; ord[b] = t; }
+        for (int h = 0; h < d; h++) {
+            int jh = ord[h];
+            ids[h] = hsh[s * d + jh];
+            const uint8_t *chunk = base + (size_t)hsl[s * d + jh] * j->slice_len + s * (size_t)cs;
+            for (int b = 0; b < beta; b++)
+                memcpy(hb + (size_t)h * rb + b * sc, chunk + (size_t)pl[(s * d + jh) * beta + b] * sc, sc);
+        }
+        if (oc_clay_repair(c, ls[s], ids, d, hb, (size_t)cs, dst + s * (size_t)cs)) rc = -2;
+    }
+    memcpy(dst + ns * (size_t)cs, meta, OC_META);
+    free(hb);
+done:
+    free(ls); free(hsl); free(hsh); free(pl);
+    return rc;
+}
+
+/* node recover (network/node/src/features/spool/recover.rs:411-442): Slicer::decode from the
+ * slices in masks[o], Slicer::encode of the blob, keep slice lost[o] */
+static int recover_one(const many_job *j, int o) {
+    const oc_clay *c = j->c;
+    int av[OC_MAXQT], first = -1;
+    for (int i = 0; i < c->n; i++) { av[i] = (j->masks[o] >> i) & 1; if (av[i] && first < 0) first = i; }
+    if (first < 0) return -1;
+    const uint8_t *base = j->slices + (size_t)o * j->obj_stride;
+    const uint8_t *meta = base + (size_t)first * j->slice_len + j->slice_len - OC_META;
+    uint64_t blob_len = get_u64(meta + 8), ci = get_u64(meta + 40);
+    uint8_t *blob = (uint8_t *)malloc(blob_len ? blob_len : 1);
+    long r = oc_slicer_decode(c, 1, base, av, j->slice_len, blob);
+    if (r < 0) { free(blob); return (int)r; }
+    size_t S, ns, cs, sl = oc_slicer_geometry(c, blob_len, &S, &ns, &cs);
+    uint8_t *all = (uint8_t *)malloc((size_t)c->n * sl);
+    oc_slicer_encode(c, 1, get_u64(meta + 24), get_u64(meta + 32), ci, blob, blob_len, all);
+    memcpy(j->out + (size_t)o * j->out_stride, all + (size_t)j->lost[o] * sl, sl);
+    free(all); free(blob);
+    return 0;
+}
+
+static void *many_worker(void *arg) {
+    many_job *j = (many_job *)arg;
+    for (int o = j->tid; o < j->nobj; o += j->nthr) {
+        int r = j->kind == 0 ? decode_one(j, o) : j->kind == 1 ? repair_one(j, o) : recover_one(j, o);
+        if (r) j->status[o] = r;
+    }
+    return NULL;
+}
+
+/* kind 0 = decode, 1 = repair, 2 = recover; status[o] gets a negative code on failure (else 0).
+ * Returns the number of failed objects. */
+int oc_slicer_many(const oc_clay *c, int kind, const uint8_t *slices, size_t obj_stride, size_t slice_len,
+                   const uint32_t *masks, const int *lost, const int *down, int nobj,
+                   uint8_t *out, size_t out_stride, int nthr, int *status) {
+    if (nthr < 1) nthr = 1;
+    if (nthr > 256) nthr = 256;
+    pthread_t th[256];
+    many_job jobs[256];
+    for (int o = 0; o < nobj; o++) status[o] = 0;
+    for (int i = 0; i < nthr; i++) {
+        many_job t = {c, slices, obj_stride, slice_len, masks, lost, down, out, out_stride, nobj, i, nthr, kind, status};
+        jobs[i] = t;
+        pthread_create(&th[i], NULL, many_worker, &jobs[i]);
+    }
+    for (int i = 0; i < nthr; i++) pthread_join(th[i], NULL);
+    int bad = 0;
+    for (int o = 0; o < nobj; o++) bad += status[o] != 0;
+    return bad;
+}

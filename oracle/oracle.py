@@ -63,6 +63,7 @@ def _lib():
     L.oc_repair_plan.argtypes = [vp, i, i, ip, i, sz, sz, ip, ip, ip, ip]
     L.oc_repair_plan.restype = C.c_long
     L.oc_slicer_encode_many.argtypes = [vp, vp, sz, i, vp, sz, i]
+    L.oc_slicer_many.argtypes = [vp, i, vp, sz, sz, vp, vp, vp, i, vp, sz, i, vp]
     L.oc_generator.argtypes = [vp, vp]
     L.oc_gf_mul.argtypes = [C.c_uint8, C.c_uint8]
     L.oc_gf_mul.restype = C.c_uint8
@@ -287,6 +288,29 @@ def encode_many(clay: OracleClay, data: np.ndarray, obj_len: int, nobj: int, out
                 out_stride: int, threads: int) -> None:
     """CPU-baseline helper: Slicer::clay_default().encode over nobj objects on `threads` threads."""
     _lib().oc_slicer_encode_many(clay.h, _ptr(data), obj_len, nobj, _ptr(out), out_stride, threads)
+
+
+MANY_KIND = {"decode": 0, "repair": 1, "recover": 2}
+
+
+def slicer_many(clay: OracleClay, kind: str, slices: np.ndarray, obj_stride: int, slice_len: int, nobj: int,
+                out: np.ndarray, out_stride: int, threads: int, masks=None, lost=None, down=None) -> int:
+    """CPU-baseline helper (bench.py decode / repair / recover lines): one object per task on
+    `threads` threads, object o's 20 slices at slices[o * obj_stride:].
+      decode : Slicer::decode from the slices in masks[o] (slicer.rs:298-364) -> out (blob_len bytes);
+      repair : Slicer::repair of slice lost[o] from the plan over every slice but lost[o] and down[o]
+               (repair.rs:137-201, 97-130, 324-367) -> out (one slice);
+      recover: decode from masks[o], re-encode, keep slice lost[o] (recover.rs:411-442) -> out.
+    Returns the number of objects that failed."""
+    def arr(v, ct):
+        if v is None:
+            return None
+        a = (ct * max(1, nobj))(*[int(x) for x in v])
+        return a
+    st = (C.c_int * max(1, nobj))()
+    m, l, d = arr(masks, C.c_uint32), arr(lost, C.c_int), arr(down, C.c_int)
+    return int(_lib().oc_slicer_many(clay.h, MANY_KIND[kind], _ptr(slices), obj_stride, slice_len, m, l, d, nobj,
+                                     _ptr(out), out_stride, threads, st))
 
 
 def splitmix64_bytes(seed: int, nbytes: int) -> np.ndarray:

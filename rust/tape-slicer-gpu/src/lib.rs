@@ -101,7 +101,11 @@ pub(crate) fn repair_status(s: i32, missing: Option<SliceIndex>) -> Result<(), R
 
 /// ClayCoder (lib/slicer/src/clay.rs:13-122) with the GF(2^8) work on the GPU.  The reference's
 /// `pub clay: ClayCode` is never used outside its crate, so it has no counterpart.
-pub struct ClayCoder { pub(crate) raw: NonNull<ffi::te_clay>, pub k: usize, pub m: usize, pub d: usize }
+pub struct ClayCoder {
+    pub(crate) raw: NonNull<ffi::te_clay>, pub k: usize, pub m: usize, pub d: usize,
+    /// pinned input / slice buffers of the one-shot batch API, reused across calls
+    pub(crate) pool: PinnedPool,
+}
 // libtapeec serialises calls on one handle internally; the handle is bound to its device.
 unsafe impl Send for ClayCoder {}
 
@@ -115,7 +119,7 @@ impl ClayCoder {
         let mut p = std::ptr::null_mut();
         let r = unsafe { ffi::te_clay_new(n as u32, k as u32, d as u32, &mut p) };
         if r != 0 { fatal(r) }
-        Self { raw: NonNull::new(p).unwrap(), k, m: n - k, d }
+        Self { raw: NonNull::new(p).unwrap(), k, m: n - k, d, pool: PinnedPool::default() }
     }
 
     /// clay.rs:37-39; `packed` is ClayParams' u64 (n | k << 8 | d << 16, encoding.rs:193-197).
@@ -125,7 +129,7 @@ impl ClayCoder {
         let mut p = std::ptr::null_mut();
         let r = unsafe { ffi::te_clay_from_params(packed, &mut p) };
         if r != 0 { fatal(r) }
-        Self { raw: NonNull::new(p).unwrap(), k, m: n - k, d }
+        Self { raw: NonNull::new(p).unwrap(), k, m: n - k, d, pool: PinnedPool::default() }
     }
 
     /// The packed ClayParams of this coder (what the Slicer's profile carries).
@@ -283,20 +287,25 @@ impl OuterCoder {
 /// Page-locked host memory (te_host_alloc): the host <-> device copies of a window run from and
 /// into it at full PCIe rate, with no driver staging (VERDICT r03 missing #2: the callers' pageable
 /// `Vec`s were copied once more into a fresh pageable `Vec` per window).  Derefs to `[u8]`.
-pub struct PinnedBuf { ptr: NonNull<u8>, len: usize, cap: usize }
+pub struct PinnedBuf { ptr: NonNull<u8>, len: usize, cap: usize, init: usize }
 unsafe impl Send for PinnedBuf {}
 impl PinnedBuf {
     pub fn new(cap: usize) -> Self {
         let mut p = std::ptr::null_mut();
         let r = unsafe { ffi::te_host_alloc(cap.max(1), &mut p) };
         if r != 0 { fatal(r) }
-        Self { ptr: NonNull::new(p as *mut u8).expect("te_host_alloc"), len: 0, cap: cap.max(1) }
+        Self { ptr: NonNull::new(p as *mut u8).expect("te_host_alloc"), len: 0, cap: cap.max(1), init: 0 }
     }
     pub fn capacity(&self) -> usize { self.cap }
-    /// Visible length (<= capacity); new bytes are zero-filled only when the buffer grows.
+    /// Visible length (<= capacity).  Bytes are zero-filled once, the first time they become
+    /// visible (past the buffer's high-water mark); a reused buffer keeps its old contents, which
+    /// the caller (or the library, which writes every output byte) overwrites.
     pub fn set_len(&mut self, len: usize) {
         assert!(len <= self.cap);
-        if len > self.len { unsafe { std::ptr::write_bytes(self.ptr.as_ptr().add(self.len), 0, len - self.len) } }
+        if len > self.init {
+            unsafe { std::ptr::write_bytes(self.ptr.as_ptr().add(self.init), 0, len - self.init) }
+            self.init = len;
+        }
         self.len = len;
     }
 }
@@ -365,15 +374,19 @@ pub fn encode_with_proofs_batch(coder: &mut ClayCoder, objects: &[&[u8]], chunk_
     let n = coder.n();
     // the metadata suffix names this coder's own profile, not the default one
     let cfg = slicer_cfg(coder, true, 0);
-    let mut pool = PinnedPool::default();
+    // the coder's own pool: no hipHostMalloc / hipHostFree per call
+    let mut pool = std::mem::take(&mut coder.pool);
     let (data, objs, out_len) = pack_objects(coder, &mut pool, objects, chunk_index);
     let h = ffi::TE_SLICE_TREE_HEIGHT as usize;
     let mut w = EncodedWindow { slices: pool.take(out_len as usize), leaf_hashes: vec![0; objects.len() * n * 32],
                                 roots: vec![0; objects.len() * 32], proofs: vec![0; objects.len() * n * h * 32] };
-    encode_status(unsafe {
+    let r = encode_status(unsafe {
         ffi::te_encode_commit_batch_host(coder.raw.as_ptr(), &cfg, data.as_ptr(), objs.as_ptr(), objs.len(),
                                          w.slices.as_mut_ptr(), h as u32, w.leaf_hashes.as_mut_ptr(), w.roots.as_mut_ptr(),
                                          w.proofs.as_mut_ptr(), window_bytes)
-    })?;
+    });
+    pool.give(data);  // the input buffer goes back; the slices leave with the window
+    coder.pool = pool;
+    r?;
     Ok(w)
 }

@@ -113,6 +113,68 @@ static bool vmm_bufs() {
     return v;
 }
 
+// The last launches that read a shared device resource, one event per stream: each
+// call re-records its own stream's event, so a clear / free waits for the readers on EVERY stream
+// that used the resource, not only the most recent one.  Bounded: past kMax streams the events are
+// drained on the host and their slots reused (a process rarely reads one handle from > 16 streams).
+struct ReaderEvents {
+    struct E {
+        hipStream_t s = nullptr;
+        hipEvent_t ev = nullptr;
+        bool pending = false;
+    };
+    static constexpr size_t kMax = 16;
+    std::vector<E> v;
+    bool any() const {
+        for (const E &e : v)
+            if (e.pending) return true;
+        return false;
+    }
+    // after the launches on `s` that read the resource
+    hipError_t record(hipStream_t s) {
+        E *slot = nullptr;
+        for (E &e : v)
+            if (e.s == s) slot = &e;
+        if (!slot) {
+            if (v.size() >= kMax) {
+                if (hipError_t r = sync(); r != hipSuccess) return r;
+                slot = &v[0];
+                slot->s = s;
+            } else {
+                E e;
+                e.s = s;
+                if (hipError_t r = hipEventCreateWithFlags(&e.ev, hipEventDisableTiming); r != hipSuccess) return r;
+                v.push_back(e);
+                slot = &v.back();
+            }
+        }
+        hipError_t r = hipEventRecord(slot->ev, s);
+        if (r == hipSuccess) slot->pending = true;
+        return r;
+    }
+    // stream `s` waits (on the device) for every reader on the other streams
+    hipError_t wait(hipStream_t s) const {
+        for (const E &e : v)
+            if (e.pending && e.s != s)
+                if (hipError_t r = hipStreamWaitEvent(s, e.ev, 0); r != hipSuccess) return r;
+        return hipSuccess;
+    }
+    // the host waits for every reader (before the resource is freed)
+    hipError_t sync() {
+        for (E &e : v)
+            if (e.pending) {
+                if (hipError_t r = hipEventSynchronize(e.ev); r != hipSuccess) return r;
+                e.pending = false;
+            }
+        return hipSuccess;
+    }
+    void destroy() {
+        for (E &e : v)
+            if (e.ev) (void)hipEventDestroy(e.ev);
+        v.clear();
+    }
+};
+
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
@@ -373,8 +435,9 @@ struct te_clay {
         uint32_t cap = 0;
         std::unordered_map<uint64_t, uint32_t> slot;
         uint32_t n = 0;
-        hipEvent_t used = nullptr, written = nullptr;
-        bool used_pending = false, written_pending = false;
+        ReaderEvents readers;             // the last launches that read the store, per stream
+        hipEvent_t written = nullptr;
+        bool written_pending = false;
         hipStream_t written_stream = nullptr;
         uint64_t clears = 0, grows = 0, arena_calls = 0;  // te_clay_decode_store_stats
     } dstore;
@@ -436,10 +499,10 @@ static void release_device_state(te_clay *c) {
     for (DevBuf *b : {&c->dstore.pats, &c->dstore.hdrs, &c->dstore.steps, &c->dstore.soff}) b->release();
     c->dstore.slot.clear();
     c->dstore.n = 0;
-    if (c->dstore.used) (void)hipEventDestroy(c->dstore.used);
+    c->dstore.readers.destroy();
     if (c->dstore.written) (void)hipEventDestroy(c->dstore.written);
-    c->dstore.used = c->dstore.written = nullptr;
-    c->dstore.used_pending = c->dstore.written_pending = false;
+    c->dstore.written = nullptr;
+    c->dstore.written_pending = false;
     c->dstore.written_stream = nullptr;
     c->dstore.cap = 0;
     if (c->rec_done) (void)hipEventDestroy(c->rec_done);
@@ -601,8 +664,7 @@ int te_clay_set_decode_store_cap(te_clay *c, uint32_t max_patterns) {
     std::lock_guard<std::mutex> lk(c->mu);
     te_clay::DecStore &S = c->dstore;
     if (S.cap > max_patterns) {  // shrink: the store is re-allocated at the next decode
-        if (S.used_pending) (void)hipEventSynchronize(S.used);
-        S.used_pending = false;
+        (void)S.readers.sync();
         for (DevBuf *b : {&S.pats, &S.hdrs, &S.steps, &S.soff}) b->release();
         S.cap = 0;
         S.slot.clear();
@@ -1068,10 +1130,7 @@ bool dec_store_slots(te_clay *c, const std::vector<const te_clay::DecCache *> &c
         S.arena_calls++;
         return false;
     }
-    if (!S.used) {
-        if ((rc = hip_status(hipEventCreateWithFlags(&S.used, hipEventDisableTiming)))) return false;
-        if ((rc = hip_status(hipEventCreateWithFlags(&S.written, hipEventDisableTiming)))) return false;
-    }
+    if (!S.written && (rc = hip_status(hipEventCreateWithFlags(&S.written, hipEventDisableTiming)))) return false;
     size_t fresh = 0;
     for (uint64_t k : keys) fresh += S.slot.count(k) == 0;
     if (S.n + fresh > S.cap) {
@@ -1083,8 +1142,7 @@ bool dec_store_slots(te_clay *c, const std::vector<const te_clay::DecCache *> &c
             while (cap < need) cap *= 2;
             cap = std::min(cap, cap_max);
             // the buffers are freed: every launch that read them must be done (rare: <= 6 times)
-            if (S.used_pending && (rc = hip_status(hipEventSynchronize(S.used)))) return false;
-            S.used_pending = false;
+            if ((rc = hip_status(S.readers.sync()))) return false;
             S.pats.release();
             S.hdrs.release();
             S.steps.release();
@@ -1098,7 +1156,7 @@ bool dec_store_slots(te_clay *c, const std::vector<const te_clay::DecCache *> &c
             for (uint32_t i = 0; i < cap; i++) U.soff[i] = i * kSteps;
             S.grows++;
         } else {
-            U.wait_used = S.used_pending;  // the fill waits (on the device) for the last reader
+            U.wait_used = S.readers.any();  // the fill waits (on the device) for the last reader on every stream
             S.clears++;
         }
         S.slot.clear();
@@ -1321,7 +1379,7 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     if (r) return r;
     if (in_store) {
         te_clay::DecStore &S = c->dstore;
-        if (fill.wait_used) TE_HIP(hipStreamWaitEvent(s, S.used, 0));
+        if (fill.wait_used) TE_HIP(S.readers.wait(s));
         // entries another stream filled and nobody on this stream has waited for yet
         if (S.written_pending && S.written_stream != s) TE_HIP(hipStreamWaitEvent(s, S.written, 0));
         const bool any = !fill.pats.empty() || !fill.soff.empty();
@@ -1431,10 +1489,7 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         TE_HIP(launch_gpe(a, max_er, s));
     }
     kt.stop();
-    if (in_store) {  // a later call that empties the store waits for these launches
-        TE_HIP(hipEventRecord(c->dstore.used, s));
-        c->dstore.used_pending = true;
-    }
+    if (in_store) TE_HIP(c->dstore.readers.record(s));  // a later call that empties the store waits for these launches
     return A.mark_done(s);
 }
 
@@ -3625,7 +3680,7 @@ namespace {
 constexpr size_t kOuterLutCache = 64;
 struct OuterLut {
     uint16_t *d = nullptr;
-    hipEvent_t used = nullptr;
+    ReaderEvents readers;  // the last launches that read the table, per stream
     uint64_t tick = 0;
 };
 std::mutex g_outer_mu;
@@ -3662,18 +3717,14 @@ int outer_lut(uint32_t k, uint32_t m, const std::vector<uint32_t> &recv, const s
         for (auto j = g_outer_luts.begin(); j != g_outer_luts.end(); ++j)
             if (j->second.tick < lru->second.tick) lru = j;
         DeviceGuard dg(lru->first[0]);
-        (void)hipEventSynchronize(lru->second.used);
-        (void)hipEventDestroy(lru->second.used);
+        (void)lru->second.readers.sync();  // every stream's last reader, then free
+        lru->second.readers.destroy();
         (void)hipFree(lru->second.d);
         g_outer_luts.erase(lru);
     }
     OuterLut L;
     TE_HIP(hipMalloc((void **)&L.d, lut.size() * sizeof(uint16_t)));
     if (hipError_t e = hipMemcpy(L.d, lut.data(), lut.size() * sizeof(uint16_t), hipMemcpyHostToDevice); e != hipSuccess) {
-        (void)hipFree(L.d);
-        return hip_status(e);
-    }
-    if (hipError_t e = hipEventCreateWithFlags(&L.used, hipEventDisableTiming); e != hipSuccess) {
         (void)hipFree(L.d);
         return hip_status(e);
     }
@@ -3727,7 +3778,7 @@ int te_outer_decode(uint32_t k, uint32_t n, const uint8_t *const *chunks, size_t
         KTimer kt(nullptr);
         r = hip_status(launch_rs16_decode(a, 1, nullptr));
         kt.stop();
-        if (r == TE_OK) r = hip_status(hipEventRecord(L->used, nullptr));
+        if (r == TE_OK) r = hip_status(L->readers.record(nullptr));
     }
     for (uint32_t i = 0; i < nm && r == TE_OK; i++)
         r = hip_status(hipMemcpy(out + (size_t)miss[i] * chunk_bytes, d + sh + (size_t)i * chunk_bytes, chunk_bytes,
@@ -3802,7 +3853,7 @@ int outer_decode_segs(uint32_t k, uint32_t n, const uint8_t *const *d_chunks, ui
             kt.stop();
             if (r) return r;
         }
-        if ((r = hip_status(hipEventRecord(L->used, s)))) return r;
+        if ((r = hip_status(L->readers.record(s)))) return r;
     }
     return r;
 }

@@ -1,0 +1,96 @@
+// hbm_probe.hip -- measurement only (libtecprobe.so, loaded by bench.py; not part of libtapeec).
+//
+// The box's own ceiling for the encode's byte mix, measured in the same process just before the
+// timed region (two box types ran the same binary at 0.41 and 0.48 of the 8 TB/s
+// spec, with identical reported clocks, so the bench line carries what THIS box's HBM does with
+// the encode's exact traffic).  The mix is the encode's algorithmic bytes of one step: the batch's
+// object bytes read once and its slice bytes written once (4.29 GB in, 14.64 GB out for 1024 x
+// 4 MiB), with no compute, no barriers and no re-reads:
+//   shape 0 ("blocks"): every workgroup streams a contiguous input range and a contiguous output
+//                       range in whole 1 KiB wave-blocks (16 B per lane, nt stores);
+//   shape 1 ("rows"):   the same, but the output walks 1,430-byte rows from a 2-aligned start, two
+//                       store instructions per row -- the slices' sub-chunk rows, as the encode
+//                       kernel writes them.
+// A kernel can at best reach the "blocks" figure; "rows" is what the slices' row shape alone costs.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool ROWS>
+__global__ void __launch_bounds__(256) mix_kernel(const uint8_t *in, uint64_t in_per_wg, uint8_t *out,
+                                                  uint64_t out_per_wg, uint32_t *sink) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint8_t *src = in + (uint64_t)blockIdx.x * in_per_wg;
+    uint8_t *dst = out + (uint64_t)blockIdx.x * out_per_wg;
+    const __amdgpu_buffer_rsrc_t rb =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(src), 0, (int)in_per_wg, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wb = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)out_per_wg, 0x00020000);
+    const uint32_t nin = (uint32_t)(in_per_wg / 1024);
+    const uint32_t nout = (uint32_t)(ROWS ? (out_per_wg - 2) / 1430 : out_per_wg / 1024);
+    const uint32_t iters = (nin + 3) / 4;
+    u32x4 acc = {0, 0, 0, 0};
+    const u32x4 v = {lane, wv, 7u, 9u};
+    for (uint32_t it = 0; it < iters; it++) {
+        const uint32_t blk = it * 4 + wv;
+        if (blk < nin) acc ^= __builtin_amdgcn_raw_buffer_load_b128(rb, (int)(blk * 1024 + lane * 16), 0, 0);
+        // this iteration's share of the output, in proportion (reads : writes as in the encode)
+        const uint32_t w0 = (uint32_t)((uint64_t)it * nout / iters), w1 = (uint32_t)((uint64_t)(it + 1) * nout / iters);
+        for (uint32_t b = w0 + wv; b < w1; b += 4) {
+            if constexpr (ROWS) {
+                const uint32_t base = 2 + b * 1430u;
+                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)(lane * 16), (int)base, 2);
+                const uint32_t o1 = lane < 25 ? 1024u + 16u * lane : (lane == 25 ? 1430u - 16u : 0x80000000u);
+                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)o1, (int)base, 2);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)(b * 1024 + lane * 16), 0, 2);
+            }
+        }
+    }
+    if (acc.x == 0x12345678u && acc.y == 3u) sink[0] = acc.z;  // keeps the loads; never true for the bench input
+}
+
+uint32_t *g_sink = nullptr;
+
+}  // namespace
+
+// Average ms per launch of the mix over `reps` launches (after one untimed launch), on `stream`.
+// in/out: device buffers of >= in_bytes / out_bytes; out is overwritten with junk.  `wgs`
+// workgroups of 256 threads split both ranges evenly (per-workgroup ranges under 2 GiB).
+// Returns 0, or a HIP error code.
+extern "C" int tec_probe_encode_mix(const void *in, uint64_t in_bytes, void *out, uint64_t out_bytes, int shape,
+                                    int wgs, int reps, void *stream, float *ms_out) {
+    if (!in || !out || wgs <= 0 || reps <= 0 || !ms_out) return (int)hipErrorInvalidValue;
+    hipStream_t s = (hipStream_t)stream;
+    if (!g_sink) {
+        hipError_t e = hipMalloc(&g_sink, 64);
+        if (e != hipSuccess) return (int)e;
+    }
+    const uint64_t ipw = (in_bytes / (uint64_t)wgs) & ~(uint64_t)1023;
+    const uint64_t opw = shape ? out_bytes / (uint64_t)wgs : (out_bytes / (uint64_t)wgs) & ~(uint64_t)1023;
+    if (ipw >= (1ull << 31) || opw >= (1ull << 31)) return (int)hipErrorInvalidValue;
+    auto launch = [&] {
+        if (shape)
+            hipLaunchKernelGGL(mix_kernel<true>, dim3(wgs), dim3(256), 0, s, (const uint8_t *)in, ipw, (uint8_t *)out,
+                               opw, g_sink);
+        else
+            hipLaunchKernelGGL(mix_kernel<false>, dim3(wgs), dim3(256), 0, s, (const uint8_t *)in, ipw, (uint8_t *)out,
+                               opw, g_sink);
+    };
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return (int)hipErrorUnknown;
+    launch();
+    (void)hipEventRecord(e0, s);
+    for (int r = 0; r < reps; r++) launch();
+    (void)hipEventRecord(e1, s);
+    hipError_t e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipGetLastError();
+    float ms = 0;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *ms_out = ms / (float)reps;
+    return (int)e;
+}

@@ -304,18 +304,27 @@ void Pool::stop() {
 int Pool::set_threads(int n) {
     if (n <= 0) n = default_threads();
     {
-        // resize only an idle pool (the stream writers hold no queued work)
+        // resize only an idle pool (the stream writers hold no queued work), and hold new
+        // submissions until the new workers run: a gate released between stop() and start()
+        // would queue tasks no worker takes
         std::unique_lock<std::mutex> g(m_);
-        cv_gate_.wait(g, [&] { return gates_.empty() && work_.empty() && busy_ == 0; });
+        cv_gate_.wait(g, [&] { return !resizing_ && gates_.empty() && work_.empty() && busy_ == 0; });
+        resizing_ = true;
     }
     stop();
-    start(n);
+    {
+        std::lock_guard<std::mutex> g(m_);
+        start(n);
+        resizing_ = false;
+    }
+    cv_gate_.notify_all();
     return 0;
 }
 
 void Pool::submit_after(hipEvent_t ev, int device, std::vector<std::function<void()>> tasks) {
     {
-        std::lock_guard<std::mutex> g(m_);
+        std::unique_lock<std::mutex> g(m_);
+        cv_gate_.wait(g, [&] { return !resizing_; });
         gates_.push_back(Gate{ev, device, std::move(tasks)});
     }
     cv_gate_.notify_all();

@@ -103,6 +103,7 @@ class Pool {
     std::vector<std::thread> workers_;
     std::thread gate_;
     bool quit_ = false;
+    bool resizing_ = false;  // set_threads in progress: submit_after waits (no task may land between stop and start)
     int nthreads_ = 0;
     int busy_ = 0;
     double rate_ = 1.5e9;

@@ -135,3 +135,37 @@ def test_decode_store_default_cap_holds_2048_random_objects():
     assert torch.equal(a, d_in) and torch.equal(b, d_in)
     assert st1["arena_calls"] == 0 and st1["capacity"] == 16384 and st1["used"] == nobj, st1
     assert st2 == st1, (st1, st2)
+
+
+def test_decode_store_clear_after_readers_on_two_streams():
+    """the store is emptied and refilled by a call on a third stream while calls on two
+    other streams may still be reading it.  The refill must wait for the last reader on EVERY
+    stream (per-stream reader events), not only the most recent one: call A (3,000 objects over 300
+    patterns) on s1, call B (200 other patterns) on s2, then call C (300 fresh patterns, overflowing
+    a 512-slot store) on s3, with no host wait between them -- all three outputs exact."""
+    import torch
+    s = T.Slicer.clay_default()
+    s.coder.set_decode_jit("off")
+    s.coder.set_decode_store_cap(512)
+    nobj = 3000
+    d_in, d_out, g, per, meta = _encoded(torch, s, nobj, 15)
+    rnd = random.Random(16)
+    pa = _masks(rnd, 300)
+    pb = _masks(rnd, 200, exclude=frozenset(pa))
+    pc = _masks(rnd, 300, exclude=frozenset(pa) | frozenset(pb))
+    ma = [pa[i % 300] for i in range(nobj)]
+    s1, s2, s3 = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    oa = torch.zeros(nobj * L, dtype=torch.uint8, device="cuda")
+    ob = torch.zeros(200 * L, dtype=torch.uint8, device="cuda")
+    oc = torch.zeros(300 * L, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    batch.decode_batch(s, d_out, [(i * per, g.slice_len, ma[i], i * L) for i in range(nobj)], meta * nobj, oa, s1)
+    batch.decode_batch(s, d_out, [(i * per, g.slice_len, pb[i], i * L) for i in range(200)], meta * 200, ob, s2)
+    st1 = s.coder.decode_store_stats()
+    batch.decode_batch(s, d_out, [(i * per, g.slice_len, pc[i], i * L) for i in range(300)], meta * 300, oc, s3)
+    st2 = s.coder.decode_store_stats()
+    torch.cuda.synchronize()
+    assert st2["clears"] == st1["clears"] + 1, (st1, st2)  # C emptied the store
+    assert torch.equal(oa, d_in)
+    assert torch.equal(ob, d_in[:200 * L])
+    assert torch.equal(oc, d_in[:300 * L])
