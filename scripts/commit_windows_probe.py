@@ -16,6 +16,30 @@ import tape_amd as T  # noqa: E402
 from tape_amd import batch  # noqa: E402
 
 
+def threads_cpu():
+    """Per-thread CPU ticks (utime + stime) of this process, from /proc."""
+    out = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            f = open(f"/proc/self/task/{tid}/stat").read().rsplit(")", 1)[1].split()
+            out[tid] = (int(f[11]) + int(f[12]), open(f"/proc/self/task/{tid}/comm").read().strip())
+        except OSError:
+            pass
+    return out
+
+
+def idle_cpu(sec=0.5):
+    """CPU the process burns while the caller sleeps (a spinning thread shows here): ticks per
+    second of wall time, and the busiest threads."""
+    a = threads_cpu()
+    time.sleep(sec)
+    b = threads_cpu()
+    hz = os.sysconf("SC_CLK_TCK")
+    d = sorted(((b[t][0] - a.get(t, (0,))[0]) / hz / sec, b[t][1], t) for t in b)
+    busy = [(round(x, 2), n, t) for x, n, t in d[::-1][:4] if x > 0.02]
+    return round(sum(x for x, _, _ in d), 2), busy
+
+
 def main():
     m, L = 1024, 4 << 20
     s = T.Slicer.clay_default()
@@ -42,14 +66,31 @@ def main():
          ("device", 2), ("device", 8), ("host", 4), ("device", 4), ("auto", 4))
     if os.environ.get("SEQ"):  # e.g. SEQ=device:2,auto:4
         seq = tuple((h, int(g)) for h, g in (x.split(":") for x in os.environ["SEQ"].split(",")))
+    d_probe = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+
+    def d2h_rate(dst):
+        """plain D2H of 1 GiB into the front of a pinned host buffer (GB/s)"""
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dst[:1 << 30].copy_(d_probe, non_blocking=True)
+        torch.cuda.synchronize()
+        return round((1 << 30) / (time.perf_counter() - t0) / 1e9, 1)
+
+    fresh = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
+    print({"d2h_GBps_h_out": d2h_rate(h_out), "d2h_GBps_fresh": d2h_rate(fresh)}, flush=True)
     for hashing, gib in seq:
         batch.set_commit_hashing(hashing)
         batch.encode_commit_batch_host(s, h_in, objs, h_out, leaf, root, proof, window_bytes=gib << 30)
         t = time.perf_counter()
+        c0 = time.process_time()
         for _ in range(2):
             batch.encode_commit_batch_host(s, h_in, objs, h_out, leaf, root, proof, window_bytes=gib << 30)
         el = time.perf_counter() - t
-        res.append({"hashing": hashing, "group_GiB": gib, "GiBps": round(2 * m * L / el / 2**30, 3)})
+        cpu = time.process_time() - c0
+        idle, busy = idle_cpu()
+        res.append({"hashing": hashing, "group_GiB": gib, "GiBps": round(2 * m * L / el / 2**30, 3),
+                    "cpu_cores_during": round(cpu / el, 2), "cpu_cores_idle_after": idle, "busy_threads_idle": busy,
+                    "d2h_GBps_h_out_after": d2h_rate(h_out), "d2h_GBps_fresh_after": d2h_rate(fresh)})
         print(res[-1], flush=True)
     batch.set_commit_hashing("auto")
     print(json.dumps({"probe": "encode_commit_batch_host group size / hashing", "runs": res}), flush=True)

@@ -45,10 +45,18 @@ namespace dstage {
 #ifndef TEC_DEC_LATE_LD
 #define TEC_DEC_LATE_LD 1  // 1: a step's loads for the next step issued after its own are consumed (r04: random 5.47 vs 5.52-5.55 ms, recover 3.89 vs 3.94-3.96; 115 VGPRs instead of 127); 0: at the step's start
 #endif
+#ifndef TEC_DEC_WPL
+#define TEC_DEC_WPL 1  // words per lane: each lane decodes WPL words (columns 4w.. of WPL row segments) with one step's control
+#endif
+#ifndef TEC_DEC_WPE_WIDE
+#define TEC_DEC_WPE_WIDE 2  // waves per SIMD the register budget is cut for when WPL > 1
+#endif
 #ifndef TEC_DEC_TAB_LDS
 #define TEC_DEC_TAB_LDS 0  // 1: v_perm tables staged in LDS (broadcast reads; r04 A/B: random 5.52 vs 5.51 ms, recover 4.12 vs 3.93); 0: scalar-loaded
 #endif
 constexpr int kMaxG = TEC_DEC_MAXG;
+constexpr int kWpl = TEC_DEC_WPL;
+static_assert(kWpl >= 1 && kWpl <= 2 && (kWpl == 1 || TEC_DEC_DIRECT), "WPL > 1 needs direct output");
 constexpr uint32_t kTabDw = 8;  // LDS dwords per v_perm table (5 used; 32-byte aligned for one b128 + one b32 read)
 __host__ __device__ constexpr uint32_t tab_lds_bytes(int nk) { return TEC_DEC_TAB_LDS ? (uint32_t)(2 * kRepQ - nk) * nk * kTabDw * 4u : 0u; }
 constexpr uint32_t kMaxLdsRows = 64;  // 2 x staging + zero + trash + slots (G = 6: 96 KB)
@@ -61,10 +69,13 @@ static_assert(kPft.u_c[0] == 3 && kPft.u_p[0] == 2 && kPft.c_u[0] == 3 && kPft.c
 static_assert(kPft.t_u[0] == kPft.t_u[1] && kPft.t_p[0] == kPft.t_p[1] && (kPft.t_u[0] ^ kPft.t_p[0]) == 1,
               "type-1 C = t (U ^ Cp) ^ Cp");
 
-template <int NK, int G>
-__global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs a) {
+template <int NK, int G, int WPL = kWpl>
+__global__ void __launch_bounds__(G * 64, WPL > 1 ? TEC_DEC_WPE_WIDE : TEC_DEC_WPE) dec_stage_kernel(DecArgs a) {
     constexpr int NE = 2 * kRepQ - NK;  // padded patterns: every other node erased
-    constexpr uint32_t RS = G * 256u;
+    // a lane owns WPL words: word k of lane t is column group (seg * WPL + k) * G * 64 + t, so each
+    // load instruction still reads G * 256 contiguous bytes; LDS slot rows and scratch rows hold
+    // the WPL word groups side by side (RSW bytes each)
+    constexpr uint32_t RSW = G * 256u, RS = RSW * WPL;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint8_t *const lds8 = reinterpret_cast<uint8_t *>(lds);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -81,13 +92,18 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
     const DecStepP *prog = a.steps + ((cU32 *)(uintptr_t)a.step_off)[J.pattern];
     const uint32_t sc = a.sc, wps = a.words_per_stripe;
     const uint32_t seg0 = seg * RS, lseg = min(RS, sc - seg0);
-    uint32_t w = seg * G * 64u + threadIdx.x;
-    if (w >= wps) w = wps - 1;
-    const uint32_t col = w * 4u;
     // a word whose high half lies past the sub-chunk (sc = 2 mod 4) loads the dword 2 bytes
     // earlier and rotates: the last row of the last slice may end the buffer
-    const bool tailw = col + 4u > sc;
-    const uint32_t vcol = tailw ? col - 2u : col, vsh = tailw ? 2u : 0u;
+    uint32_t vcol[WPL], vsh[WPL];
+#pragma unroll
+    for (int k = 0; k < WPL; k++) {
+        uint32_t w = (seg * WPL + k) * G * 64u + threadIdx.x;
+        if (w >= wps) w = wps - 1;  // words past the stripe alias the last (same values, same bytes)
+        const uint32_t col = w * 4u;
+        const bool tailw = col + 4u > sc;
+        vcol[k] = tailw ? col - 2u : col;
+        vsh[k] = tailw ? 2u : 0u;
+    }
     const uint32_t in_range = (uint32_t)(a.n * a.in_stride);  // host-checked < 2^31
     const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc((void *)J.in, 0, (int)in_range, 0x00020000);
     // data chunk x at out + x * out_stride, trimmed to the stripe's share of the object
@@ -102,20 +118,23 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
     for (int j = 0; j < NK; j++) kbase[j] = __builtin_amdgcn_readlane(sl_lane, H.knode[j]);
     // raw input word (the tail-word rotation is applied where the value is consumed, so a load
     // inside a branch has no use inside it)
-    auto ldraw = [&](uint32_t so) -> uint32_t {
+    auto ldraw = [&](uint32_t so, int k) -> uint32_t {
         if (TEC_DEC_ABLATE & 8) return so;
-        return __builtin_amdgcn_raw_buffer_load_b32(rs_in, (int)vcol, (int)so, 0);
+        return __builtin_amdgcn_raw_buffer_load_b32(rs_in, (int)vcol[k], (int)so, 0);
     };
-    auto ldopt = [&](uint32_t so) -> uint32_t { return (TEC_DEC_COND_LD && so == 0x80000000u) ? 0u : ldraw(so); };
+    auto ldopt = [&](uint32_t so, int k) -> uint32_t { return (TEC_DEC_COND_LD && so == 0x80000000u) ? 0u : ldraw(so, k); };
     // staged rows need each word's bytes in column order (the tail lane's load rotated); direct
     // output stores every word back where it was loaded, and all the arithmetic is byte-wise, so
     // the loaded order is kept throughout
-    auto rot = [&](uint32_t v) { return TEC_DEC_DIRECT ? v : __builtin_amdgcn_alignbyte(v, v, vsh); };
+    auto rot = [&](uint32_t v, int k) { return TEC_DEC_DIRECT ? v : __builtin_amdgcn_alignbyte(v, v, vsh[k]); };
     // LDS rows: two staging buffers of max_out rows (a step stages into buffer st & 1, so one
     // barrier per step suffices), a zero row, a trash row, then the lane-private slots
     const uint32_t mo = TEC_DEC_DIRECT ? 0u : H.max_out, zrow = 2u * mo, trow = zrow + 1u, srow0 = zrow + 2u;
-    auto lds_at = [&](uint32_t off) -> uint32_t * { return reinterpret_cast<uint32_t *>(lds8 + off + col_local); };
-    *lds_at(zrow * RS) = 0u;  // lane-private: read back only by this lane
+    auto lds_at = [&](uint32_t off, int k) -> uint32_t * {
+        return reinterpret_cast<uint32_t *>(lds8 + off + (uint32_t)k * RSW + col_local);
+    };
+#pragma unroll
+    for (int k = 0; k < WPL; k++) *lds_at(zrow * RS, k) = 0u;  // lane-private: read back only by this lane
     // flush: staging row i -> data chunk x at the item's plane, the whole row by one wave
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t nb = lseg >> 4, tail = lseg & 15u;
@@ -210,31 +229,39 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
     };
     // one decoded word (in the lane's load order) to its row at `off` (uniform), at the lane's
     // load column vcol; a row across the stripe's output share is written byte by byte there
-    auto put_out = [&](uint32_t off, uint32_t wv_) {
+    auto put_out = [&](uint32_t off, uint32_t wv_, int k) {
         if (off == kDrop) return;
         if (off + sc <= olen) {
-            __builtin_amdgcn_raw_buffer_store_b32(wv_, rs_out, (int)vcol, (int)off, TEC_DEC_ST_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(wv_, rs_out, (int)vcol[k], (int)off, TEC_DEC_ST_AUX);
         } else {
 #pragma unroll
-            for (uint32_t k = 0; k < 4u; k++)  // bytes past out_len fail the range check
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(wv_ >> (8u * k)), rs_out, (int)(vcol + k), (int)off, 0);
+            for (uint32_t b = 0; b < 4u; b++)  // bytes past out_len fail the range check
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(wv_ >> (8u * b)), rs_out, (int)(vcol[k] + b), (int)off, 0);
         }
     };
 
-    uint32_t own[NK], part[NK], tkp[NE];
+    uint32_t own[WPL][NK], part[WPL][NK], tkp[WPL][NE];
     auto load_known = [&](uint32_t x) {
         const uint32_t zs = (W(x, kDpHdr) & 0xffu) * sc;
         const uint32_t vin = vec_in(x);
 #pragma unroll
         for (int j = 0; j < NK; j++) {
-            own[j] = ldraw(kbase[j] + zs);
-            part[j] = ldopt(W(vin, kDpKd + j));
+            const uint32_t so = W(vin, kDpKd + j);
+#pragma unroll
+            for (int k = 0; k < WPL; k++) {
+                own[k][j] = ldraw(kbase[j] + zs, k);
+                part[k][j] = ldopt(so, k);
+            }
         }
     };
     auto load_tkp = [&](uint32_t x) {
         const uint32_t vin = vec_in(x);
 #pragma unroll
-        for (int e = 0; e < NE; e++) tkp[e] = ldopt(W(vin, kDpEd + e));
+        for (int e = 0; e < NE; e++) {
+            const uint32_t so = W(vin, kDpEd + e);
+#pragma unroll
+            for (int k = 0; k < WPL; k++) tkp[k][e] = ldopt(so, k);
+        }
     };
     auto load_step = [&](uint32_t x) {
         load_known(x);
@@ -242,22 +269,33 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
     };
     // scratch loads of a step, issued after the previous step's scratch stores (lane-private
     // addresses: program order within the lane is the only ordering needed)
-    uint32_t ksc[NK], esc[NE];
+    uint32_t ksc[WPL][NK], esc[WPL][NE];
     auto load_scr = [&](uint32_t x) {
         const uint32_t vs = vec_scr(x);
         if (TEC_DEC_ABLATE & 1) {
-            for (int j = 0; j < NK; j++) ksc[j] = 0;
-            for (int e = 0; e < NE; e++) esc[e] = 0;
+            for (int k = 0; k < WPL; k++) {
+                for (int j = 0; j < NK; j++) ksc[k][j] = 0;
+                for (int e = 0; e < NE; e++) esc[k][e] = 0;
+            }
             return;
         }
-        auto ld = [&](uint32_t so) -> uint32_t {
-            return (TEC_DEC_COND_LD && so == 0x80000000u) ? 0u
-                                                          : __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)col_local, (int)so, 0);
+        auto ld = [&](uint32_t so, int k) -> uint32_t {
+            return (TEC_DEC_COND_LD && so == 0x80000000u)
+                       ? 0u
+                       : __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)(col_local + (uint32_t)k * RSW), (int)so, 0);
         };
 #pragma unroll
-        for (int j = 0; j < NK; j++) ksc[j] = ld(W(vs, kDpKd + j));
+        for (int j = 0; j < NK; j++) {
+            const uint32_t so = W(vs, kDpKd + j);
 #pragma unroll
-        for (int e = 0; e < NE; e++) esc[e] = ld(W(vs, kDpEd + e));
+            for (int k = 0; k < WPL; k++) ksc[k][j] = ld(so, k);
+        }
+#pragma unroll
+        for (int e = 0; e < NE; e++) {
+            const uint32_t so = W(vs, kDpEd + e);
+#pragma unroll
+            for (int k = 0; k < WPL; k++) esc[k][e] = ld(so, k);
+        }
     };
 
     const uint32_t nsteps = H.nsteps;
@@ -266,22 +304,29 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
     load_scr(w_cur);
     for (uint32_t st = 0; st < nsteps; st++) {
         const uint32_t w_nn = ldw(st + 2);
-        uint32_t cown[NK], cpart[NK], ctkp[NE];
+        uint32_t cown[WPL][NK], cpart[WPL][NK], ctkp[WPL][NE];
 #pragma unroll
-        for (int j = 0; j < NK; j++) cown[j] = rot(own[j]), cpart[j] = rot(part[j]);
+        for (int k = 0; k < WPL; k++) {
 #pragma unroll
-        for (int e = 0; e < NE; e++) ctkp[e] = rot(tkp[e]);
+            for (int j = 0; j < NK; j++) cown[k][j] = rot(own[k][j], k), cpart[k][j] = rot(part[k][j], k);
+#pragma unroll
+            for (int e = 0; e < NE; e++) ctkp[k][e] = rot(tkp[k][e], k);
+        }
         if constexpr (!TEC_DEC_LATE_LD) load_step(w_nxt);  // blank step: every partner load dropped
         if constexpr (TEC_DEC_PRIO) __builtin_amdgcn_s_setprio(TEC_DEC_PRIO);
         // ---- uncouple the known nodes: dropped loads read 0, a non-slot partner reads the zero
         // row, a red node masks the PFT term ----
         const uint32_t vsl = vec_slot(w_cur);
-        Sel sel[NK];
+        Sel sel[WPL][NK];
 #pragma unroll
         for (int j = 0; j < NK; j++) {
-            const uint32_t p = cpart[j] ^ ksc[j] ^ *lds_at(W(vsl, kDpKd + j));
             const uint32_t mred = (W(w_cur, kDpKd + j) >> 28) == kKnRed ? 0u : ~0u;
-            sel[j] = Sel(cown[j] ^ (xt(cown[j] ^ p) & mred));
+            const uint32_t sl_off = W(vsl, kDpKd + j);
+#pragma unroll
+            for (int k = 0; k < WPL; k++) {
+                const uint32_t p = cpart[k][j] ^ ksc[k][j] ^ *lds_at(sl_off, k);
+                sel[k][j] = Sel(cown[k][j] ^ (xt(cown[k][j] ^ p) & mred));
+            }
         }
         // known data rows: copies (staging is double-buffered, so any time in the step)
         const uint32_t sbase = (st & 1u) * mo;
@@ -289,11 +334,15 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
             if (TEC_DEC_DIRECT) {
                 const uint32_t ok = vec_out(w_cur >> 16, w_cur);
 #pragma unroll
-                for (int j = 0; j < NK; j++) put_out(W(ok, kDpKd + j), cown[j]);
+                for (int j = 0; j < NK; j++) {
+                    const uint32_t o = W(ok, kDpKd + j);
+#pragma unroll
+                    for (int k = 0; k < WPL; k++) put_out(o, cown[k][j], k);
+                }
             } else {
                 const uint32_t lk = dst_lds(w_cur >> 16, sbase);
 #pragma unroll
-                for (int j = 0; j < NK; j++) *lds_at(W(lk, kDpKd + j)) = cown[j];
+                for (int j = 0; j < NK; j++) *lds_at(W(lk, kDpKd + j), 0) = cown[0][j];
             }
         }
         // TEC_DEC_LATE_LD: the next step's known-row loads once this step's are consumed (no second
@@ -301,46 +350,63 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
         if constexpr (TEC_DEC_LATE_LD != 0) load_known(w_nxt);
         // pair partners' U (read before this step's writes: a location may be rewritten from its
         // consumer step on)
-        uint32_t pu[NE];
-#pragma unroll
-        for (int e = 0; e < NE; e++) pu[e] = esc[e] ^ *lds_at(W(vsl, kDpEd + e));
-        // ---- MDS-solve the erased U's the program needs ----
-        uint32_t acc[NE];
+        uint32_t pu[WPL][NE];
 #pragma unroll
         for (int e = 0; e < NE; e++) {
-            acc[e] = 0;
+            const uint32_t sl_off = W(vsl, kDpEd + e);
+#pragma unroll
+            for (int k = 0; k < WPL; k++) pu[k][e] = esc[k][e] ^ *lds_at(sl_off, k);
+        }
+        // ---- MDS-solve the erased U's the program needs ----
+        uint32_t acc[WPL][NE];
+#pragma unroll
+        for (int e = 0; e < NE; e++) {
+#pragma unroll
+            for (int k = 0; k < WPL; k++) acc[k][e] = 0;
             if ((W(w_cur, kDpEd + e) >> 28) == kErSkip) continue;
             if (TEC_DEC_ABLATE & 2) {
 #pragma unroll
-                for (int j = 0; j < NK; j++) acc[e] ^= sel[j].s0 + e;
+                for (int k = 0; k < WPL; k++)
+#pragma unroll
+                    for (int j = 0; j < NK; j++) acc[k][e] ^= sel[k][j].s0 + e;
                 continue;
             }
             // known inputs in pairs: 3 perms and 1.5 XOR3 per product, plus a v_mov per 3-bit perm
             // when both table halves are SGPRs (one SGPR operand per VALU instruction on gfx9; the
-            // tables in LDS instead, one broadcast ds_read_b128 per product, measured 30 % slower)
+            // tables in LDS instead, one broadcast ds_read_b128 per product, measured 30 % slower);
+            // the WPL words of a lane share each table
             if constexpr (TEC_DEC_TAB_LDS != 0) {
                 const uint32_t *tr = lds + tab_dw + (uint32_t)e * NK * kTabDw;
                 auto tq = [&](int j) { return *reinterpret_cast<const u32x4 *>(tr + j * kTabDw); };
 #pragma unroll
                 for (int j = 0; j + 1 < NK; j += 2) {
                     const u32x4 p = tq(j), q = tq(j + 1);
-                    acc[e] = perm_mul2_acc(acc[e], sel[j], p.x, p.y, p.z, p.w, tr[j * kTabDw + 4], sel[j + 1], q.x, q.y, q.z,
-                                           q.w, tr[(j + 1) * kTabDw + 4]);
+                    const uint32_t p4 = tr[j * kTabDw + 4], q4 = tr[(j + 1) * kTabDw + 4];
+#pragma unroll
+                    for (int k = 0; k < WPL; k++)
+                        acc[k][e] = perm_mul2_acc(acc[k][e], sel[k][j], p.x, p.y, p.z, p.w, p4, sel[k][j + 1], q.x, q.y,
+                                                  q.z, q.w, q4);
                 }
                 if (NK & 1) {
                     const u32x4 p = tq(NK - 1);
-                    acc[e] = perm_mul_acc(acc[e], sel[NK - 1], p.x, p.y, p.z, p.w, tr[(NK - 1) * kTabDw + 4]);
+                    const uint32_t p4 = tr[(NK - 1) * kTabDw + 4];
+#pragma unroll
+                    for (int k = 0; k < WPL; k++) acc[k][e] = perm_mul_acc(acc[k][e], sel[k][NK - 1], p.x, p.y, p.z, p.w, p4);
                 }
                 continue;
             }
 #pragma unroll
             for (int j = 0; j + 1 < NK; j += 2)
-                acc[e] = perm_mul2_acc(acc[e], sel[j], D[e][j].t[0], D[e][j].t[1], D[e][j].t[2], D[e][j].t[3], D[e][j].t[4],
-                                       sel[j + 1], D[e][j + 1].t[0], D[e][j + 1].t[1], D[e][j + 1].t[2], D[e][j + 1].t[3],
-                                       D[e][j + 1].t[4]);
+#pragma unroll
+                for (int k = 0; k < WPL; k++)
+                    acc[k][e] = perm_mul2_acc(acc[k][e], sel[k][j], D[e][j].t[0], D[e][j].t[1], D[e][j].t[2], D[e][j].t[3],
+                                              D[e][j].t[4], sel[k][j + 1], D[e][j + 1].t[0], D[e][j + 1].t[1],
+                                              D[e][j + 1].t[2], D[e][j + 1].t[3], D[e][j + 1].t[4]);
             if (NK & 1)
-                acc[e] = perm_mul_acc(acc[e], sel[NK - 1], D[e][NK - 1].t[0], D[e][NK - 1].t[1], D[e][NK - 1].t[2],
-                                      D[e][NK - 1].t[3], D[e][NK - 1].t[4]);
+#pragma unroll
+                for (int k = 0; k < WPL; k++)
+                    acc[k][e] = perm_mul_acc(acc[k][e], sel[k][NK - 1], D[e][NK - 1].t[0], D[e][NK - 1].t[1],
+                                             D[e][NK - 1].t[2], D[e][NK - 1].t[3], D[e][NK - 1].t[4]);
         }
         // ---- writes: lane A of a word is its general destination (known: kout; erased: the
         // park location; eo: ed0), B and C the staging-only ed1 / epd ----
@@ -351,29 +417,40 @@ __global__ void __launch_bounds__(G * 64, TEC_DEC_WPE) dec_stage_kernel(DecArgs 
         const uint32_t oa = TEC_DEC_DIRECT ? vec_out(w_cur, w_cur) : kDrop;
         const uint32_t ob = TEC_DEC_DIRECT ? vec_out(w_cur >> 10, w_cur) : kDrop;
         const uint32_t oc = TEC_DEC_DIRECT ? vec_out(w_cur >> 20, w_cur) : kDrop;
-        auto put_a = [&](int i, uint32_t v) {
-            *lds_at(W(la, i)) = v;
+        auto put_a = [&](int i, uint32_t v, int k) {
+            *lds_at(W(la, i), k) = v;
             const uint32_t so = W(sa, i);
-            if (so != kDrop) __builtin_amdgcn_raw_buffer_store_b32(v, rs_scr, (int)col_local, (int)so, 0);
+            if (so != kDrop)
+                __builtin_amdgcn_raw_buffer_store_b32(v, rs_scr, (int)(col_local + (uint32_t)k * RSW), (int)so, 0);
         };
 #pragma unroll
         for (int e = 0; e < NE; e++) {
             const uint32_t ek = W(w_cur, kDpEd + e) >> 28;
             if (ek == kErRed) {
-                *lds_at(W(la, kDpEo + e)) = acc[e];
-                if (TEC_DEC_DIRECT) put_out(W(oa, kDpEo + e), acc[e]);
+#pragma unroll
+                for (int k = 0; k < WPL; k++) {
+                    *lds_at(W(la, kDpEo + e), k) = acc[k][e];
+                    if (TEC_DEC_DIRECT) put_out(W(oa, kDpEo + e), acc[k][e], k);
+                }
             } else if (ek == kErType1) {
-                const uint32_t c = mulc(kPft.t_u[0], acc[e] ^ ctkp[e]) ^ ctkp[e];
-                put_a(kDpEo + e, c);
-                *lds_at(W(lb, kDpEo + e)) = c;
-                if (TEC_DEC_DIRECT) put_out(W(oa, kDpEo + e), c), put_out(W(ob, kDpEo + e), c);
+#pragma unroll
+                for (int k = 0; k < WPL; k++) {
+                    const uint32_t c = mulc(kPft.t_u[0], acc[k][e] ^ ctkp[k][e]) ^ ctkp[k][e];
+                    put_a(kDpEo + e, c, k);
+                    *lds_at(W(lb, kDpEo + e), k) = c;
+                    if (TEC_DEC_DIRECT) put_out(W(oa, kDpEo + e), c, k), put_out(W(ob, kDpEo + e), c, k);
+                }
             } else if (ek == kErPark) {
-                put_a(kDpEd + e, acc[e]);
+#pragma unroll
+                for (int k = 0; k < WPL; k++) put_a(kDpEd + e, acc[k][e], k);
             } else if (ek == kErFinish) {
-                const uint32_t c0 = pft3(acc[e], pu[e]), c1 = pft3(pu[e], acc[e]);
-                *lds_at(W(la, kDpEo + e)) = c0;
-                *lds_at(W(lc, kDpEo + e)) = c1;
-                if (TEC_DEC_DIRECT) put_out(W(oa, kDpEo + e), c0), put_out(W(oc, kDpEo + e), c1);
+#pragma unroll
+                for (int k = 0; k < WPL; k++) {
+                    const uint32_t c0 = pft3(acc[k][e], pu[k][e]), c1 = pft3(pu[k][e], acc[k][e]);
+                    *lds_at(W(la, kDpEo + e), k) = c0;
+                    *lds_at(W(lc, kDpEo + e), k) = c1;
+                    if (TEC_DEC_DIRECT) put_out(W(oa, kDpEo + e), c0, k), put_out(W(oc, kDpEo + e), c1, k);
+                }
             }
         }
         if constexpr (TEC_DEC_LATE_LD != 0) load_tkp(w_nxt);
@@ -420,15 +497,20 @@ uint32_t decode_stage_g(uint32_t words_per_stripe) {
     return groups < (uint32_t)dstage::kMaxG ? groups : (uint32_t)dstage::kMaxG;
 }
 
+// workgroups per stripe: groups of 64 words, g * WPL of them per workgroup
+static uint32_t decode_stage_wgs(uint32_t words_per_stripe) {
+    const uint32_t groups = (words_per_stripe + 63) / 64, g = decode_stage_g(words_per_stripe);
+    return (groups + g * dstage::kWpl - 1) / (g * dstage::kWpl);
+}
+
 size_t decode_stage_scratch_bytes(const DecArgs &a) {
-    const uint32_t groups = (a.words_per_stripe + 63) / 64, g = decode_stage_g(a.words_per_stripe);
-    const uint32_t wgs = (groups + g - 1) / g;
-    return (size_t)a.njobs * wgs * (a.nscratch_max ? a.nscratch_max : 1) * g * 256u;
+    const uint32_t g = decode_stage_g(a.words_per_stripe), wgs = decode_stage_wgs(a.words_per_stripe);
+    return (size_t)a.njobs * wgs * (a.nscratch_max ? a.nscratch_max : 1) * g * 256u * dstage::kWpl;
 }
 
 template <int NK, int G>
 static hipError_t launch_dec_g(const DecArgs &a, uint64_t blocks, hipStream_t s) {
-    const size_t lds = (size_t)a.lds_rows * G * 256u + dstage::tab_lds_bytes(NK);
+    const size_t lds = (size_t)a.lds_rows * G * 256u * dstage::kWpl + dstage::tab_lds_bytes(NK);
     hipError_t e = ensure_dyn_lds(reinterpret_cast<const void *>(dstage::dec_stage_kernel<NK, G>), lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((dstage::dec_stage_kernel<NK, G>), dim3((uint32_t)blocks), dim3(G * 64), lds, s, a);
@@ -448,8 +530,8 @@ hipError_t launch_decode_stage(DecArgs a, hipStream_t s) {
     if (a.lds_rows == 0 || a.lds_rows > dstage::kMaxLdsRows || a.sc < 8 || !a.scratch || a.n != 2u * kRepQ ||
         !decode_stage_k((int)a.nk))
         return hipErrorInvalidValue;
-    const uint32_t groups = (a.words_per_stripe + 63) / 64, g = decode_stage_g(a.words_per_stripe);
-    a.wgs_per_stripe = (groups + g - 1) / g;
+    const uint32_t g = decode_stage_g(a.words_per_stripe);
+    a.wgs_per_stripe = decode_stage_wgs(a.words_per_stripe);
     const uint64_t blocks = (uint64_t)a.njobs * a.wgs_per_stripe;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     switch (a.nk) {

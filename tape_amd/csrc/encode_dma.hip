@@ -48,7 +48,21 @@ constexpr int kCap = 5;  // flush rows per wave per step
 constexpr int kStoreLag = 30;
 static_assert(kStoreLag <= 3 * 2 * kCap && kStoreLag < 64, "stores older than 3 steps must have landed");
 constexpr uint32_t kDrop = 0x80000000u;    // offset past every resource: the range check drops it
-constexpr int kStAux = 2;                  // slice stores: nt
+#ifndef TEC_DMA_ST_AUX
+#define TEC_DMA_ST_AUX 2
+#endif
+constexpr int kStAux = TEC_DMA_ST_AUX;     // slice stores: nt
+// DMA issue shape (measurement variants): 0 = packed (7 own rows in 10 instructions, 9 partner rows
+// in 13); 1 = one instruction pair per row, each input row's SECOND touch (own row read after it
+// was a partner, or partner after own, or a red row's only touch) non-temporal and its first touch
+// default policy, so the rows a later plane re-reads are the ones the caches keep; 2 = per row,
+// every row default policy
+#ifndef TEC_DMA_ROWPOL
+#define TEC_DMA_ROWPOL 1
+#endif
+#ifndef TEC_DMA_L2NT
+#define TEC_DMA_L2NT 1  // level-2 partner rows (parity read back from the slices) non-temporal
+#endif
 // (r01-r03 timing variants of this kernel -- direct stores, DMA orders, priorities, ablations,
 // occupancy probes -- live in the measurement copy scripts/kbench_encode_dma.hip)
 
@@ -146,13 +160,26 @@ __device__ __forceinline__ u32x4 rsrc(const void *p, uint32_t nrec) {
 // One LDS-DMA piece: lane l's 16 bytes at (voff + soff) of the resource land at LDS
 // lds + 16 l.  Inline asm on purpose (see the header): the compiler neither counts it nor
 // orders LDS reads behind it; the kernel waits with explicit vmcnt + barrier.
+// cache policy of a second-touch (or only-touch) DMA row (TEC_DMA_ROWPOL 1) / a level-2 partner
+#ifndef TEC_DMA_NT_SEL
+#define TEC_DMA_NT_SEL 0
+#endif
+#if TEC_DMA_NT_SEL == 1
+#define TEC_DMA_NT_POL "sc0 nt"
+#elif TEC_DMA_NT_SEL == 2
+#define TEC_DMA_NT_POL "sc1 nt"
+#elif TEC_DMA_NT_SEL == 3
+#define TEC_DMA_NT_POL "sc0 sc1 nt"
+#else
+#define TEC_DMA_NT_POL "nt"
+#endif
 template <bool NT>
 __device__ __forceinline__ void dma16(u32x4 rs, uint32_t voff, uint32_t soff, uint32_t lds) {
     uint32_t keep;
     if constexpr (NT)
         asm volatile(
             "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-            "buffer_load_dwordx4 %1, %2, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+            "buffer_load_dwordx4 %1, %2, %4 offen " TEC_DMA_NT_POL " lds\n\ts_mov_b32 m0, %0"
             : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds), "s"(soff) : "memory");
     else
         asm volatile(
@@ -250,7 +277,40 @@ __global__ void __launch_bounds__(kWaves * 64, 4) enc_dma_kernel(EncArgs a) {
     // x != z0: the input chunk z0 at level 1, node z0's slice at level 2 (level-1 parity rows
     // and parked U, written >= 8 steps earlier -- complete by the vmcnt waits below; nt loads
     // skip this CU's L1).
+    // per-row pieces (TEC_DMA_ROWPOL): lane l's block l of the row (first instruction) and block
+    // 64 + l (second, lanes < RB - 64)
+    const uint32_t rvo0 = 16u * lane, rvo1 = lane < RB - 64u ? 16u * (64u + lane) : kDrop;
+    auto issue_rows = [&](uint32_t tp, uint32_t slot) {
+        const uint32_t nz0 = tp / kQ, ns = tp - nz0 * kQ;
+        const bool lvl2 = nz0 >= (uint32_t)K;
+        const uint32_t so_own = src_al + tp * sc;
+        const uint32_t so_pbase = lvl2 ? slice_off(nz0) + ns * sc : src_al + nz0 * cs + ns * sc;
+        auto piece = [&](bool from_dst, bool nt, uint32_t so, uint32_t ld) {
+            so = __builtin_amdgcn_readfirstlane(so);
+            ld = __builtin_amdgcn_readfirstlane(lds0 + ld);
+            const u32x4 rs = from_dst ? rs_dst : rs_src;
+            if (nt) dma16<true>(rs, rvo0, so, ld);
+            else dma16<false>(rs, rvo0, so, ld);
+            if (rvo1 != kDrop) {
+                if (nt) dma16<true>(rs, rvo1, so, ld + 1024u);
+                else dma16<false>(rs, rvo1, so, ld + 1024u);
+            }
+        };
+#pragma unroll
+        for (int x = 0; x < K; x++)  // own rows: a second touch unless its partner read is still ahead
+            piece(false, TEC_DMA_ROWPOL == 1 && (lvl2 || (uint32_t)x <= nz0), so_own + x * cs, slot + x * RW);
+#pragma unroll
+        for (int p = 0; p < 9; p++) {
+            const uint32_t x = (uint32_t)p + ((uint32_t)p >= nz0 ? 1u : 0u);
+            piece(lvl2, TEC_DMA_ROWPOL == 1 && (lvl2 ? TEC_DMA_L2NT != 0 : x < nz0), so_pbase + x * kQ * sc,
+                  slot + kPartBase + p * RW);
+        }
+    };
     auto issue_dma = [&](uint32_t tp, uint32_t slot) {
+        if constexpr (TEC_DMA_ROWPOL != 0) {
+            issue_rows(tp, slot);
+            return;
+        }
         const uint32_t nz0 = tp / kQ, ns = tp - nz0 * kQ;
         const uint32_t so_own = __builtin_amdgcn_readfirstlane(src_al + tp * sc);
         const bool lvl2 = nz0 >= (uint32_t)K;
@@ -290,7 +350,10 @@ __global__ void __launch_bounds__(kWaves * 64, 4) enc_dma_kernel(EncArgs a) {
         // the compute waves' B2 / B1 (the ring slot of plane z is free after B1 of z)
         issue_dma(0, 0);
         issue_dma(1, kSlotBytes);
-        asm volatile("s_waitcnt vmcnt(23)\n\ts_barrier" ::: "memory");  // plane 0 landed
+        if constexpr (TEC_DMA_ROWPOL != 0)
+            asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");  // plane 0 landed (16 rows x 2)
+        else
+            asm volatile("s_waitcnt vmcnt(23)\n\ts_barrier" ::: "memory");  // plane 0 landed
         for (uint32_t z = 0; z < (uint32_t)(kQ * kQ); z++) {
             lds_barrier();                                  // B2
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // plane z + 1 landed

@@ -630,8 +630,16 @@ hipError_t launch_gather(const CopyJob *jobs, uint32_t njobs, hipStream_t s) {
 
 bool encode_rows_supported(int n, int k, int d) { return n == 20 && d == k + 9 && (k == 7 || k == 10); }
 
+// waves per workgroup: every column group of the stripe when they fit (kMaxG), or at most
+// a.groups_per_wg when the caller set it (small batches: more, shorter workgroups per stripe)
+static uint32_t stage_g(const EncArgs &a) {
+    uint32_t g = a.groups_per_stripe < (uint32_t)stage::kMaxG ? a.groups_per_stripe : (uint32_t)stage::kMaxG;
+    if (a.groups_per_wg && a.groups_per_wg < g) g = a.groups_per_wg;
+    return g;
+}
+
 size_t encode_rows_scratch_bytes(const EncArgs &a) {
-    const uint32_t g = a.groups_per_stripe < (uint32_t)stage::kMaxG ? a.groups_per_stripe : (uint32_t)stage::kMaxG;
+    const uint32_t g = stage_g(a);
     const uint32_t wgs = (a.groups_per_stripe + g - 1) / g;
     return (size_t)a.njobs * wgs * stage::kScratchRows * g * 256u;
 }
@@ -648,7 +656,7 @@ hipError_t launch_stage_g(const EncArgs &a, uint64_t blocks, hipStream_t s) {
 template <int K, bool MASKED>
 hipError_t launch_stage(EncArgs a, hipStream_t s) {
     if (a.njobs == 0) return hipSuccess;
-    const uint32_t g = a.groups_per_stripe < (uint32_t)stage::kMaxG ? a.groups_per_stripe : (uint32_t)stage::kMaxG;
+    const uint32_t g = stage_g(a);
     a.groups_per_wg = g;
     a.wgs_per_stripe = (a.groups_per_stripe + g - 1) / g;
     a.stripes_per_wg = 1;

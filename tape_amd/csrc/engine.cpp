@@ -19,6 +19,7 @@
 #include <functional>
 #include <thread>
 #include <atomic>
+#include <condition_variable>
 #include "../../include/tape_ec.h"
 #include "kernels.hpp"
 #include "sha256.hpp"
@@ -38,6 +39,16 @@ thread_local char g_last_error[256] = "";
 const bool g_no_dma_encode = [] {
     const char *e = tec_knob("TEC_ENCODE_KERNEL");
     return e && strcmp(e, "stage") == 0;
+}();
+
+// Small per-call encodes (te_slicer_encode / te_clay_encode): a call of at most TEC_ENC_SMALL 1 MB
+// stripes may run the staged kernel with one wave per workgroup (six workgroups per stripe).
+// Measured slower (r05 trace of --mode percall: 438 us per 4 MiB object against 296 us for the
+// LDS-DMA kernel -- a lone stripe is bound by the 100-plane chain's latency, not its work per
+// step), so it is off (0); measurement only.
+const uint32_t g_enc_small = [] {
+    const char *e = tec_knob("TEC_ENC_SMALL");
+    return e ? (uint32_t)atoi(e) : 0u;
 }();
 
 // TEC_REPAIR_KERNEL=stage keeps the folded repair kernel off (measurement / cross-check only)
@@ -175,6 +186,85 @@ struct ReaderEvents {
     }
 };
 
+// Host memcpy fan-out for the per-call entry points: a few persistent threads (plus the caller)
+// copy a list of segments, big segments split into 64 KiB pieces.  Used to gather a call's
+// scattered host buffers (Slicer::repair's d helper buffers, repair.rs:340-354) into one pinned
+// staging buffer -- one H2D instead of one driver-staged copy per helper -- and to scatter the
+// result back into the caller's (pageable) buffer.
+class CopyPool {
+  public:
+    struct Seg {
+        void *dst;
+        const void *src;
+        size_t len;
+    };
+    static CopyPool &get() {
+        static CopyPool *p = new CopyPool();  // never destroyed (workers outlive static destructors)
+        return *p;
+    }
+    void run(const std::vector<Seg> &segs) {
+        constexpr size_t kPiece = 64 << 10;
+        std::lock_guard<std::mutex> one(call_mu_);  // one job at a time
+        pieces_.clear();
+        size_t total = 0;
+        for (const Seg &g : segs)
+            for (size_t o = 0; o < g.len; o += kPiece) {
+                const size_t l = std::min(kPiece, g.len - o);
+                pieces_.push_back({static_cast<uint8_t *>(g.dst) + o, static_cast<const uint8_t *>(g.src) + o, l});
+                total += l;
+            }
+        if (pieces_.size() <= 1 || total < (128u << 10) || workers_.empty()) {  // not worth waking anyone
+            for (const Seg &g : pieces_) memcpy(g.dst, g.src, g.len);
+            return;
+        }
+        next_.store(0);
+        done_.store(0);
+        {
+            std::lock_guard<std::mutex> g(m_);
+            gen_++;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> g(m_);
+        cv_done_.wait(g, [&] { return done_.load() == pieces_.size(); });
+    }
+
+  private:
+    CopyPool() {
+        const int n = std::max(0, std::min(3, hh::default_threads() - 1));
+        for (int i = 0; i < n; i++)
+            workers_.emplace_back([this] {
+                uint64_t seen = 0;
+                for (;;) {
+                    {
+                        std::unique_lock<std::mutex> g(m_);
+                        cv_.wait(g, [&] { return gen_ != seen; });
+                        seen = gen_;
+                    }
+                    work();
+                }
+            });
+        for (auto &t : workers_) t.detach();
+    }
+    void work() {
+        for (;;) {
+            const size_t i = next_.fetch_add(1);
+            if (i >= pieces_.size()) return;
+            memcpy(pieces_[i].dst, pieces_[i].src, pieces_[i].len);
+            if (done_.fetch_add(1) + 1 == pieces_.size()) {
+                std::lock_guard<std::mutex> g(m_);
+                cv_done_.notify_all();
+            }
+        }
+    }
+    std::mutex call_mu_, m_;
+    std::condition_variable cv_, cv_done_;
+    std::vector<Seg> pieces_;
+    std::atomic<size_t> next_{0}, done_{0};
+    uint64_t gen_ = 0;
+    std::vector<std::thread> workers_;
+};
+
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
@@ -255,9 +345,10 @@ struct DevBuf {
     void release() { (void)free_(); }
 };
 
-struct HostBuf {  // pinned staging for descriptor uploads
+struct HostBuf {  // pinned staging (descriptor uploads, the per-call entry points' host side)
     void *p = nullptr;
     size_t cap = 0;
+    uint8_t *u8() const { return static_cast<uint8_t *>(p); }
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
         if (p) (void)hipHostFree(p);
@@ -396,10 +487,12 @@ struct te_clay {
     hipStream_t stream = nullptr;  // for the synchronous host-buffer entry points
     Arena enc, dec, rep, rec;
     DevBuf io_in, io_out;          // staging for host-buffer entry points
+    HostBuf hio_in, hio_out;       // their page-locked host side (te_slicer_repair's gather / scatter)
     // te_recover_batch_device workspaces (decoded objects, re-encoded slices); `rec_done` is
     // recorded after the last launch that reads them, on `rec_stream`
     DevBuf rec_blob, rec_slices;
     hipEvent_t rec_done = nullptr;
+    hipEvent_t io_ev[2] = {};      // te_slicer_repair: the two halves of the result's D2H
     bool rec_pending = false;
     hipStream_t rec_stream = nullptr;
     // te_encode_batch_host pipeline: kPipe slots, each with its own stream, descriptor arena
@@ -494,6 +587,8 @@ static void release_device_state(te_clay *c) {
     c->rec.release();
     c->io_in.release();
     c->io_out.release();
+    c->hio_in.release();
+    c->hio_out.release();
     c->rec_blob.release();
     c->rec_slices.release();
     for (DevBuf *b : {&c->dstore.pats, &c->dstore.hdrs, &c->dstore.steps, &c->dstore.soff}) b->release();
@@ -505,6 +600,8 @@ static void release_device_state(te_clay *c) {
     c->dstore.written_pending = false;
     c->dstore.written_stream = nullptr;
     c->dstore.cap = 0;
+    for (hipEvent_t &e : c->io_ev)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
     if (c->rec_done) (void)hipEventDestroy(c->rec_done);
     c->rec_done = nullptr;
     dec_jit_free(c->jit);  // joins compiles in flight; every stream is drained above
@@ -828,7 +925,7 @@ using StripeSel = std::function<uint32_t(size_t, size_t)>;
 
 int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, const te_object *objs,
                    size_t nobj, uint8_t *d_out, hipStream_t s, bool raw, Arena *arena = nullptr,
-                   const StripeSel &keep = StripeSel()) {
+                   const StripeSel &keep = StripeSel(), bool per_call = false) {
     const ClayHost &h = c->h;
     const int n = h.n;
     const int rotated = cfg ? cfg->rotated : 0;
@@ -913,8 +1010,13 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
     auto fast_path = [&](const Launch &L) {
         return c->fast_encode && !L.key.odd && (uint64_t)n * L.key.slice_len < 0x7fffffffull;
     };
+    size_t total_stripes = 0;
+    for (const Launch &L : launches) total_stripes += L.count;
+    // a small per-call encode (every chunk kept): the staged kernel with one wave per workgroup
+    const bool small = per_call && !keep && total_stripes <= g_enc_small;
     auto dma_path = [&](const Launch &L) {
-        return fast_path(L) && encode_dma_supported(n, h.k, (uint32_t)(L.key.cs / h.alpha)) && !g_no_dma_encode;
+        return fast_path(L) && encode_dma_supported(n, h.k, (uint32_t)(L.key.cs / h.alpha)) && !g_no_dma_encode &&
+               !small;
     };
     size_t scratch_bytes = 0;
     for (const Launch &L : launches) {
@@ -923,6 +1025,7 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
         EncArgs a{};
         a.njobs = (uint32_t)L.count;
         a.groups_per_stripe = (wps + 63) / 64;
+        a.groups_per_wg = small ? 1u : 0u;
         scratch_bytes = std::max(scratch_bytes, encode_rows_scratch_bytes(a));
     }
     uint8_t *scratch = nullptr;
@@ -974,6 +1077,7 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
             a.jobs = A.at<EncJob>(L.off);
             a.njobs = (uint32_t)L.count;
             a.groups_per_stripe = (wps + 63) / 64;
+            a.groups_per_wg = small ? 1u : 0u;
             a.words_per_stripe = wps;
             a.cs = cs;
             a.sc = sc;
@@ -3131,7 +3235,8 @@ int te_slicer_encode(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *data, 
     TE_HIP(c->io_out.ensure(total));
     if (len) TE_HIP(hipMemcpyAsync(c->io_in.p, data, len, hipMemcpyHostToDevice, c->stream));
     te_object o{0, len, 0, cfg->chunk_index};
-    r = encode_enqueue(c, cfg, c->io_in.as<uint8_t>(), &o, 1, c->io_out.as<uint8_t>(), c->stream, false);
+    r = encode_enqueue(c, cfg, c->io_in.as<uint8_t>(), &o, 1, c->io_out.as<uint8_t>(), c->stream, false, nullptr,
+                       StripeSel(), true);
     if (r) return r;
     TE_HIP(hipMemcpyAsync(slices, c->io_out.p, total, hipMemcpyDeviceToHost, c->stream));
     TE_HIP(hipStreamSynchronize(c->stream));
@@ -3155,7 +3260,8 @@ int te_clay_encode(te_clay *c, const uint8_t *data, size_t len, uint8_t *chunks,
     TE_HIP(hipMemcpyAsync(c->io_in.p, data, len, hipMemcpyHostToDevice, c->stream));
     te_object o{0, len, 0, 0};
     te_slicer_cfg cfg{0, TE_ENCODING_CLAY, TE_CLAY_DEFAULT_PARAMS, 0};
-    r = encode_enqueue(c, &cfg, c->io_in.as<uint8_t>(), &o, 1, c->io_out.as<uint8_t>(), c->stream, true);
+    r = encode_enqueue(c, &cfg, c->io_in.as<uint8_t>(), &o, 1, c->io_out.as<uint8_t>(), c->stream, true, nullptr,
+                       StripeSel(), true);
     if (r) return r;
     TE_HIP(hipMemcpyAsync(chunks, c->io_out.p, total, hipMemcpyDeviceToHost, c->stream));
     TE_HIP(hipStreamSynchronize(c->stream));
@@ -3405,15 +3511,47 @@ int te_slicer_repair(te_clay *c, const te_repair_plan *p, const uint8_t *const *
     if (r) return r;
     TE_HIP(c->io_in.ensure(total + 16));
     TE_HIP(c->io_out.ensure(out_bytes));
-    for (uint32_t sl = 0; sl < p->n; sl++)
-        if (need[sl])
-            TE_HIP(hipMemcpyAsync(c->io_in.as<uint8_t>() + off[sl], helper_data[sl], need[sl], hipMemcpyHostToDevice,
+    // the d helpers' buffers gathered into page-locked staging (parallel memcpy), one H2D; the
+    // repaired slice back through staging: per call two DMA copies, not d + 1 driver-staged ones
+    TE_HIP(c->hio_in.ensure(total + 16));
+    TE_HIP(c->hio_out.ensure(out_bytes));
+    // In pieces of ~1/4 of the bytes: piece i's H2D runs while piece i + 1 is gathered.
+    {
+        std::vector<CopyPool::Seg> segs;
+        uint64_t done = 0, piece_end = 0;
+        const uint64_t quarter = (total + 3) / 4;
+        auto flush = [&](uint64_t upto) -> int {
+            CopyPool::get().run(segs);
+            segs.clear();
+            TE_HIP(hipMemcpyAsync(c->io_in.as<uint8_t>() + done, c->hio_in.u8() + done, upto - done, hipMemcpyHostToDevice,
                                   c->stream));
+            done = upto;
+            return TE_OK;
+        };
+        for (uint32_t sl = 0; sl < p->n; sl++) {
+            if (!need[sl]) continue;
+            segs.push_back({c->hio_in.u8() + off[sl], helper_data[sl], need[sl]});
+            piece_end = off[sl] + need[sl];
+            if (piece_end - done >= quarter && (r = flush(piece_end))) return r;
+        }
+        if (!segs.empty() && (r = flush(piece_end))) return r;
+    }
     RepItem it{p, off.data(), 0, metadata};
     r = repair_enqueue(c, c->io_in.as<uint8_t>(), &it, 1, c->io_out.as<uint8_t>(), c->stream);
     if (r) return r;
-    TE_HIP(hipMemcpyAsync(out, c->io_out.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
-    TE_HIP(hipStreamSynchronize(c->stream));
+    // the result in two halves: the first half's scatter overlaps the second half's D2H
+    for (hipEvent_t &e : c->io_ev)
+        if (!e) TE_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    const size_t half = (out_bytes / 2 + 4095) & ~(size_t)4095;
+    const size_t h0 = std::min(half, out_bytes), h1 = out_bytes - h0;
+    TE_HIP(hipMemcpyAsync(c->hio_out.p, c->io_out.p, h0, hipMemcpyDeviceToHost, c->stream));
+    TE_HIP(hipEventRecord(c->io_ev[0], c->stream));
+    if (h1) TE_HIP(hipMemcpyAsync(c->hio_out.u8() + h0, c->io_out.as<uint8_t>() + h0, h1, hipMemcpyDeviceToHost, c->stream));
+    TE_HIP(hipEventRecord(c->io_ev[1], c->stream));
+    TE_HIP(hipEventSynchronize(c->io_ev[0]));
+    CopyPool::get().run({{out, c->hio_out.p, h0}});
+    TE_HIP(hipEventSynchronize(c->io_ev[1]));
+    if (h1) CopyPool::get().run({{out + h0, c->hio_out.u8() + h0, h1}});
     return TE_OK;
 }
 
