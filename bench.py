@@ -92,14 +92,14 @@ KERNELS = {
     "repair": ["tec::rfold::rep_fold_kernel"],  # every folded instance (lost column x known set)
     "decode": ["tec_dec_fixed"],  # the pattern kernels (dec_rtc.cpp); random patterns / --decode-jit off: table-driven
     "commit": ["tec::commit::leaf_kernel", "tec::commit::tree_kernel"],
-    "recover": ["tec::dstage::dec_stage_kernel<7, 2>"],  # the fused decode writing only the lost slices
+    "recover": ["tec::dstage::dec_stage_kernel<7, 2, 1>"],  # the fused decode writing only the lost slices
 }
 
 
 def kernel_names(mode: str, decode_jit: str = "async", pattern: str = "worst") -> list:
     # random survivor sets serve ~1 object per pattern: no pattern reaches a compiled kernel
     if mode == "decode" and (decode_jit == "off" or pattern == "random"):
-        return ["tec::dstage::dec_stage_kernel<7, 2>"]
+        return ["tec::dstage::dec_stage_kernel<7, 2, 1>"]
     return KERNELS.get(mode, [])
 
 

@@ -28,6 +28,42 @@ def threads_cpu():
     return out
 
 
+class ClockSampler:
+    """Samples the GPU's current sclk / mclk DPM level (sysfs pp_dpm_*) every 5 ms while active."""
+
+    def __init__(self):
+        import threading
+        p = torch.cuda.get_device_properties(0)
+        self.base = f"/sys/bus/pci/devices/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        self.samples = []
+        self.on = False
+        self.th = threading.Thread(target=self.loop, daemon=True)
+        self.th.start()
+
+    def cur(self, fn):
+        try:
+            for l in open(os.path.join(self.base, fn)):
+                if l.strip().endswith("*"):
+                    return l.split(":")[1].strip().rstrip("*").strip()
+        except OSError:
+            return None
+
+    def loop(self):
+        while True:
+            if self.on:
+                self.samples.append((self.cur("pp_dpm_sclk"), self.cur("pp_dpm_mclk"), self.cur("pp_dpm_fclk")))
+            time.sleep(0.005)
+
+    def start(self):
+        self.samples = []
+        self.on = True
+
+    def stop(self):
+        self.on = False
+        import collections
+        return dict(collections.Counter(self.samples).most_common(4))
+
+
 def idle_cpu(sec=0.5):
     """CPU the process burns while the caller sleeps (a spinning thread shows here): ticks per
     second of wall time, and the busiest threads."""
@@ -77,20 +113,24 @@ def main():
         return round((1 << 30) / (time.perf_counter() - t0) / 1e9, 1)
 
     fresh = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
+    clk = ClockSampler()
     print({"d2h_GBps_h_out": d2h_rate(h_out), "d2h_GBps_fresh": d2h_rate(fresh)}, flush=True)
     for hashing, gib in seq:
         batch.set_commit_hashing(hashing)
         batch.encode_commit_batch_host(s, h_in, objs, h_out, leaf, root, proof, window_bytes=gib << 30)
         t = time.perf_counter()
         c0 = time.process_time()
+        clk.start()
         for _ in range(2):
             batch.encode_commit_batch_host(s, h_in, objs, h_out, leaf, root, proof, window_bytes=gib << 30)
         el = time.perf_counter() - t
+        clocks = clk.stop()
         cpu = time.process_time() - c0
         idle, busy = idle_cpu()
         res.append({"hashing": hashing, "group_GiB": gib, "GiBps": round(2 * m * L / el / 2**30, 3),
                     "cpu_cores_during": round(cpu / el, 2), "cpu_cores_idle_after": idle, "busy_threads_idle": busy,
-                    "d2h_GBps_h_out_after": d2h_rate(h_out), "d2h_GBps_fresh_after": d2h_rate(fresh)})
+                    "d2h_GBps_h_out_after": d2h_rate(h_out), "d2h_GBps_fresh_after": d2h_rate(fresh),
+                    "clocks_sclk_mclk_fclk": {" / ".join(map(str, k)): v for k, v in clocks.items()}})
         print(res[-1], flush=True)
     batch.set_commit_hashing("auto")
     print(json.dumps({"probe": "encode_commit_batch_host group size / hashing", "runs": res}), flush=True)

@@ -23,7 +23,17 @@ constexpr uint64_t kLeafBlocksPerLaunch = 1536;  // ~3.5 ms of one stream's SHA-
 // last store it, and the last stores the digest.  Long slices are hashed in several launches of
 // about kLeafBlocksPerLaunch blocks (a 30 ms launch holds up any copy queued behind it
 // on a shared hardware queue; ~3 ms launches do not).
+#ifndef TEC_LEAF_PRIO
+#define TEC_LEAF_PRIO 3
+#endif
 __global__ void __launch_bounds__(64) leaf_kernel(CommitArgs a, uint64_t b0, uint64_t b1) {
+    // Wave priority (r05): a group's hashing runs beside the next groups' encodes and copies, and
+    // a leaf wave is one slice's serial SHA-256 chain.  Sharing a SIMD with encode waves at equal
+    // priority it issued at a fraction of its rate, the group's hashing fell behind the encodes
+    // (one launch per group, one slice per lane: 64 waves for 205 objects), and the slot streams
+    // then waited for the hashed group buffers -- the 4 GiB-group runs at 7.5 GiB/s.
+    // The leaf waves are few; they take issue priority on their SIMDs.
+    if constexpr (TEC_LEAF_PRIO > 0) __builtin_amdgcn_s_setprio(TEC_LEAF_PRIO);
     const uint32_t total = a.nobj * a.n;
     const uint32_t gid = blockIdx.x * 64u + threadIdx.x;
     const bool live = gid < total;

@@ -45,6 +45,12 @@ namespace dstage {
 #ifndef TEC_DEC_LATE_LD
 #define TEC_DEC_LATE_LD 1  // 1: a step's loads for the next step issued after its own are consumed (r04: random 5.47 vs 5.52-5.55 ms, recover 3.89 vs 3.94-3.96; 115 VGPRs instead of 127); 0: at the step's start
 #endif
+#ifndef TEC_DEC_OWN_AUX
+#define TEC_DEC_OWN_AUX 2  // known rows' own loads non-temporal (r05 A/B: random 5.41-5.44 vs 5.49-5.53 ms, recover neutral; partner loads nt: neutral / worse)
+#endif
+#ifndef TEC_DEC_PART_AUX
+#define TEC_DEC_PART_AUX 0
+#endif
 #ifndef TEC_DEC_WPL
 #define TEC_DEC_WPL 1  // words per lane: each lane decodes WPL words (columns 4w.. of WPL row segments) with one step's control
 #endif
@@ -118,11 +124,17 @@ __global__ void __launch_bounds__(G * 64, WPL > 1 ? TEC_DEC_WPE_WIDE : TEC_DEC_W
     for (int j = 0; j < NK; j++) kbase[j] = __builtin_amdgcn_readlane(sl_lane, H.knode[j]);
     // raw input word (the tail-word rotation is applied where the value is consumed, so a load
     // inside a branch has no use inside it)
+    // cache policy of the known rows' own loads / partner loads (measurement variants)
     auto ldraw = [&](uint32_t so, int k) -> uint32_t {
         if (TEC_DEC_ABLATE & 8) return so;
-        return __builtin_amdgcn_raw_buffer_load_b32(rs_in, (int)vcol[k], (int)so, 0);
+        return __builtin_amdgcn_raw_buffer_load_b32(rs_in, (int)vcol[k], (int)so, TEC_DEC_OWN_AUX);
     };
-    auto ldopt = [&](uint32_t so, int k) -> uint32_t { return (TEC_DEC_COND_LD && so == 0x80000000u) ? 0u : ldraw(so, k); };
+    auto ldopt = [&](uint32_t so, int k) -> uint32_t {
+        if (TEC_DEC_ABLATE & 8) return so;
+        return (TEC_DEC_COND_LD && so == 0x80000000u)
+                   ? 0u
+                   : __builtin_amdgcn_raw_buffer_load_b32(rs_in, (int)vcol[k], (int)so, TEC_DEC_PART_AUX);
+    };
     // staged rows need each word's bytes in column order (the tail lane's load rotated); direct
     // output stores every word back where it was loaded, and all the arithmetic is byte-wise, so
     // the loaded order is kept throughout

@@ -19,6 +19,7 @@
 #include <functional>
 #include <thread>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include "../../include/tape_ec.h"
 #include "kernels.hpp"
@@ -492,7 +493,6 @@ struct te_clay {
     // recorded after the last launch that reads them, on `rec_stream`
     DevBuf rec_blob, rec_slices;
     hipEvent_t rec_done = nullptr;
-    hipEvent_t io_ev[2] = {};      // te_slicer_repair: the two halves of the result's D2H
     bool rec_pending = false;
     hipStream_t rec_stream = nullptr;
     // te_encode_batch_host pipeline: kPipe slots, each with its own stream, descriptor arena
@@ -600,8 +600,6 @@ static void release_device_state(te_clay *c) {
     c->dstore.written_pending = false;
     c->dstore.written_stream = nullptr;
     c->dstore.cap = 0;
-    for (hipEvent_t &e : c->io_ev)
-        if (e) (void)hipEventDestroy(e), e = nullptr;
     if (c->rec_done) (void)hipEventDestroy(c->rec_done);
     c->rec_done = nullptr;
     dec_jit_free(c->jit);  // joins compiles in flight; every stream is drained above
@@ -959,7 +957,9 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
             j.rot = rotated ? (uint32_t)((st * TE_ROTATION_STEP) % n) : 0u;
             j.dst_skew = (uint32_t)(st * cs);
             const bool masked = ((reinterpret_cast<uintptr_t>(j.src) & 3u) + j.src_len) % 4 != 0;
-            const bool odd = (reinterpret_cast<uintptr_t>(j.src) & 1u) != 0;
+            // odd source or slice bytes: the fast kernels read 2-aligned rows (and the LDS-DMA
+            // kernel's line-exact systematic stores read 2-aligned row offsets): generic kernel
+            const bool odd = ((reinterpret_cast<uintptr_t>(j.src) | reinterpret_cast<uintptr_t>(j.dst)) & 1u) != 0;
             groups[GeomKey{cs, slice_len, masked, odd}].push_back(j);
         }
         if (!raw && !keep) {
@@ -2029,12 +2029,63 @@ static void commit_plan(const CommitBatch &B, uint64_t group_bytes, uint64_t cop
 // One object's slices copied out in row pieces (host-hashed groups, pinned host output): piece p
 // is bytes [beg[p], beg[p+1]) of every slice, landed once ev[p] has completed.  The host hashing
 // tasks follow the pieces as they land instead of waiting for the whole window's D2H.
+//
+// The piece events come from a per-device pool and are waited for by polling (hipEventQuery with
+// short sleeps), not by blocking-sync waits: with one blocking-sync event created, waited for by
+// interrupt and destroyed per piece (ten per 64 MiB chunk), the SDK-shape stream slowed to
+// 7.1 GiB/s (chunk latency 33.6 ms, against 15-16 ms in a fresh process) once the process had run
+// the earlier copy-inclusive legs -- and ran 11.6 GiB/s in that same state with no pieces
+// (r05, gpurun_out/r5h).  Polling costs a worker a few microseconds per check and no interrupt.
+class EventPool {
+  public:
+    static EventPool &get(int device) {
+        static std::mutex mu;
+        static std::map<int, EventPool *> pools;
+        std::lock_guard<std::mutex> g(mu);
+        EventPool *&p = pools[device];
+        if (!p) p = new EventPool();  // never destroyed (events outlive static destructors' order)
+        return *p;
+    }
+    hipError_t acquire(hipEvent_t &e) {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            if (!free_.empty()) {
+                e = free_.back();
+                free_.pop_back();
+                return hipSuccess;
+            }
+        }
+        return hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    }
+    void release(hipEvent_t e) {
+        std::lock_guard<std::mutex> g(m_);
+        if (free_.size() < 4096) free_.push_back(e);
+        else (void)hipEventDestroy(e);
+    }
+
+  private:
+    std::mutex m_;
+    std::vector<hipEvent_t> free_;
+};
+
+// Wait for an event by polling: a short spin, then sleeps of 20 us (hashing workers waiting for
+// the next row piece of their slices).
+static hipError_t event_wait_poll(hipEvent_t e) {
+    for (int i = 0;; i++) {
+        const hipError_t r = hipEventQuery(e);
+        if (r != hipErrorNotReady) return r;
+        if (i < 16) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
 struct PieceEvents {
     int device = 0;
     std::vector<hipEvent_t> ev;
     std::vector<uint64_t> beg;
     ~PieceEvents() {
-        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+        EventPool &pool = EventPool::get(device);
+        for (hipEvent_t e : ev) pool.release(e);
     }
 };
 
@@ -2082,7 +2133,7 @@ static int copy_out_pieces(uint8_t *host, const uint8_t *dev, uint64_t slice_len
             TE_HIP(hipMemcpy2DAsync(host + off, slice_len, dev + off, slice_len, w, n, hipMemcpyDeviceToHost, s));
         }
         hipEvent_t e = nullptr;
-        TE_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync));
+        TE_HIP(EventPool::get(device).acquire(e));
         pe->ev.push_back(e);
         pe->beg.push_back(off);
         TE_HIP(hipEventRecord(e, s));
@@ -2308,7 +2359,7 @@ static int group_close_host(CommitPipe &P, OpenGroup &G, uint32_t n, uint32_t he
                         (void)hipSetDevice(pe->device);
                         const uint8_t *at[hh::kMaxLanes];
                         for (size_t p = 0; p < pe->ev.size() && !rc; p++) {
-                            rc = hip_status(hipEventSynchronize(pe->ev[p]));
+                            rc = hip_status(event_wait_poll(pe->ev[p]));
                             for (uint32_t l = 0; l < L; l++) at[l] = src[l] + pe->beg[p];
                             if (!rc) h.update(at, pe->beg[p + 1] - pe->beg[p]);
                         }
@@ -2386,13 +2437,19 @@ static int group_close(CommitPipe &P, OpenGroup &G, uint32_t n, uint32_t height,
 // launch hashes one slice per lane at ~24 MB/s per lane (715,048 B in ~29.5 ms)
 // whatever the number of slices up to ~64k of them; the host pool hashes at its measured
 // per-thread rate (SHA extensions: 1-2 GB/s) times its threads.
-// The device wins for many short slices (a batch of 4 MiB objects), the host for few long ones
-// (the SDK's 64 MiB chunks, ~9.7 MB slices, <= 4 in flight: ~0.4 s per leaf launch).
+// The device wins for very many short slices (tens of thousands of small objects' slices per
+// group); with the contended device rate (below) the host pool takes the 4 MiB objects' groups too
+// (r05: host 12.4-12.9 GiB/s against device 7.5-12.2 for 1024 x 4 MiB, every group size and
+// window size measured) and the SDK's 64 MiB chunks (~9.7 MB slices: ~0.4 s per leaf launch).
 std::atomic<int> g_commit_hashing{TE_HASH_AUTO};
 bool host_hash_wins(int mode, uint64_t streams, uint64_t max_slice, uint64_t slice_bytes) {
     if (mode == TE_HASH_HOST) return true;
     if (mode == TE_HASH_DEVICE) return false;
-    const double dev_s = (double)max_slice / 24e6 * std::max(1.0, (double)streams / 65536.0);
+    // a leaf lane hashes its slice at ~24 MB/s alone, but a group's hashing runs beside the next
+    // groups' encodes and copies, which cut that to ~8 MB/s (r05 group traces: 90-128 ms per
+    // 715 KB-slice group against 29 ms alone; with 24 MB/s here the 4 GiB groups went to the device
+    // and the one-shot call ran 7.5 GiB/s against 12.4 host-hashed)
+    const double dev_s = (double)max_slice / 8e6 * std::max(1.0, (double)streams / 65536.0);
     const hh::Pool &pool = hh::Pool::get();
     const double host_s = (double)slice_bytes / (pool.thread_rate() * pool.threads());
     return host_s < dev_s;
@@ -3515,43 +3572,19 @@ int te_slicer_repair(te_clay *c, const te_repair_plan *p, const uint8_t *const *
     // repaired slice back through staging: per call two DMA copies, not d + 1 driver-staged ones
     TE_HIP(c->hio_in.ensure(total + 16));
     TE_HIP(c->hio_out.ensure(out_bytes));
-    // In pieces of ~1/4 of the bytes: piece i's H2D runs while piece i + 1 is gathered.
-    {
-        std::vector<CopyPool::Seg> segs;
-        uint64_t done = 0, piece_end = 0;
-        const uint64_t quarter = (total + 3) / 4;
-        auto flush = [&](uint64_t upto) -> int {
-            CopyPool::get().run(segs);
-            segs.clear();
-            TE_HIP(hipMemcpyAsync(c->io_in.as<uint8_t>() + done, c->hio_in.u8() + done, upto - done, hipMemcpyHostToDevice,
-                                  c->stream));
-            done = upto;
-            return TE_OK;
-        };
-        for (uint32_t sl = 0; sl < p->n; sl++) {
-            if (!need[sl]) continue;
-            segs.push_back({c->hio_in.u8() + off[sl], helper_data[sl], need[sl]});
-            piece_end = off[sl] + need[sl];
-            if (piece_end - done >= quarter && (r = flush(piece_end))) return r;
-        }
-        if (!segs.empty() && (r = flush(piece_end))) return r;
-    }
+    std::vector<CopyPool::Seg> segs;
+    for (uint32_t sl = 0; sl < p->n; sl++)
+        if (need[sl]) segs.push_back({c->hio_in.u8() + off[sl], helper_data[sl], need[sl]});
+    CopyPool::get().run(segs);
+    TE_HIP(hipMemcpyAsync(c->io_in.p, c->hio_in.p, total, hipMemcpyHostToDevice, c->stream));
     RepItem it{p, off.data(), 0, metadata};
     r = repair_enqueue(c, c->io_in.as<uint8_t>(), &it, 1, c->io_out.as<uint8_t>(), c->stream);
     if (r) return r;
-    // the result in two halves: the first half's scatter overlaps the second half's D2H
-    for (hipEvent_t &e : c->io_ev)
-        if (!e) TE_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    const size_t half = (out_bytes / 2 + 4095) & ~(size_t)4095;
-    const size_t h0 = std::min(half, out_bytes), h1 = out_bytes - h0;
-    TE_HIP(hipMemcpyAsync(c->hio_out.p, c->io_out.p, h0, hipMemcpyDeviceToHost, c->stream));
-    TE_HIP(hipEventRecord(c->io_ev[0], c->stream));
-    if (h1) TE_HIP(hipMemcpyAsync(c->hio_out.u8() + h0, c->io_out.as<uint8_t>() + h0, h1, hipMemcpyDeviceToHost, c->stream));
-    TE_HIP(hipEventRecord(c->io_ev[1], c->stream));
-    TE_HIP(hipEventSynchronize(c->io_ev[0]));
-    CopyPool::get().run({{out, c->hio_out.p, h0}});
-    TE_HIP(hipEventSynchronize(c->io_ev[1]));
-    if (h1) CopyPool::get().run({{out + h0, c->hio_out.u8() + h0, h1}});
+    TE_HIP(hipMemcpyAsync(c->hio_out.p, c->io_out.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
+    TE_HIP(hipStreamSynchronize(c->stream));
+    // (pipelining the gather with the H2D in four pieces and the scatter with the D2H in two
+    // halves measured slower: 0.17 against 0.134-0.143 ms per 4 MiB call, r05)
+    CopyPool::get().run({{out, c->hio_out.p, out_bytes}});
     return TE_OK;
 }
 
