@@ -45,13 +45,8 @@ constexpr int kWaves = G + 1;              // six compute waves and a loader wav
 // compute waves keep at most this many stores in flight before B1, so every slice row a
 // later DMA reads back (level-2 partners, >= 8 steps later) has landed: <= 3 steps of stores
 constexpr int kCap = 5;  // flush rows per wave per step
-// Systematic rows stored line-exact by the loader wave (TEC_DMA_SYSLX, r05): see the loader below.
-#ifndef TEC_DMA_SYSLX
-#define TEC_DMA_SYSLX 1
-#endif
-constexpr int kStoreLag = TEC_DMA_SYSLX ? 24 : 30;
+constexpr int kStoreLag = 30;
 static_assert(kStoreLag <= 3 * 2 * kCap && kStoreLag < 64, "stores older than 3 steps must have landed");
-constexpr bool kSysLx = TEC_DMA_SYSLX != 0;
 constexpr uint32_t kDrop = 0x80000000u;    // offset past every resource: the range check drops it
 #ifndef TEC_DMA_ST_AUX
 #define TEC_DMA_ST_AUX 2
@@ -123,8 +118,7 @@ constexpr FlushTab make_flush_tab() {
         for (int s = 0; s < kQ; s++) {
             uint32_t items[40] = {};
             int n = 0;
-            if (!kSysLx)  // (line-exact: the loader stores the systematic rows)
-                for (int x = 0; x < K; x++) items[n++] = fitem(0x80 | x, x, -1, -1);       // systematic
+            for (int x = 0; x < K; x++) items[n++] = fitem(0x80 | x, x, -1, -1);           // systematic
             for (int r = 0; r < 3; r++) items[n++] = fitem(kRowC0 + r, K + r, -1, -1);     // nodes 7..9
             for (int i = 0; i < i0; i++) items[n++] = fitem(kRowX + i, K + i0, K + i, -1);  // C(z0, (7+i, s))
             for (int j = 0; j <= s; j++) items[n++] = fitem(kRowC1 + j, kQ + j, -1, -1);
@@ -144,12 +138,11 @@ constexpr bool flush_ok() {
     for (int t = 0; t < 4; t++)
         for (int s = 0; s < kQ; s++)
             for (int w = 0; w < G; w++)
-                if (kFlushC.w[t][s][w].n < (kSysLx ? 0u : 1u) || kFlushC.w[t][s][w].n > (uint32_t)kCap) return false;
+                if (kFlushC.w[t][s][w].n < 1 || kFlushC.w[t][s][w].n > (uint32_t)kCap) return false;
     return true;
 }
 static_assert(flush_ok(), "every wave flushes 1..kCap rows per step (>= 2 stores: the vmcnt(2) wait)");
-static_assert(kSysLx ? kFlushC.extra == 0 : (kFlushC.extra != 0 && (kFlushC.extra & 0x80u) == 0),
-              "the left-over item is a staging row (none when the loader stores the systematic rows)");
+static_assert(kFlushC.extra != 0 && (kFlushC.extra & 0x80u) == 0, "the left-over item is a staging row");
 __constant__ FlushTab kFlush = kFlushC;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -361,89 +354,10 @@ __global__ void __launch_bounds__(kWaves * 64, 4) enc_dma_kernel(EncArgs a) {
             asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");  // plane 0 landed (16 rows x 2)
         else
             asm volatile("s_waitcnt vmcnt(23)\n\ts_barrier" ::: "memory");  // plane 0 landed
-        if constexpr (!kSysLx) {
-            for (uint32_t z = 0; z < (uint32_t)(kQ * kQ); z++) {
-                lds_barrier();                                  // B2
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // plane z + 1 landed
-                lds_barrier();                                  // B1
-                if (z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, (z & 1u) * kSlotBytes);
-            }
-            return;
-        }
-        // Systematic rows, line-exact (r05).  A systematic row is a copy of its input row; the
-        // rows of a chunk are consecutive planes, one per step, so the 128-byte line a row ends in
-        // is completed by the next row one step later.  Stored as whole rows (the r04 flush), each
-        // such junction line was written by two stores a step apart -- the row-shaped store
-        // pattern that the box ceiling shows costing 20-33 % over whole lines.  Here the loader
-        // wave writes each row as the whole lines [floor128(row start), floor128(row end)) of the
-        // absolute address space: the first line's bytes before the row are the previous row's
-        // tail, kept per node in VGPRs (lanes 0..7, one 16-byte block each: `carry`), and the
-        // row's own tail line becomes the next carry.  Only a chunk's first row (plane 0: its head
-        // line belongs to the previous stripe's chunk, written by another workgroup) and last row
-        // (plane 99) write their outer partial line exactly, as before.  The bytes are read from
-        // the ring image (row-relative, 2-aligned offsets: u16 reads) after B1 -- the compute
-        // waves are done with the slot and have patched the data-end word -- and stored before
-        // the slot's next DMA is issued, so the loader's wait for that DMA also covers them.
-        const uint32_t dst_mod = (uint32_t)reinterpret_cast<uintptr_t>(J.dst) & 127u;
-        u32x4 carry[K];
-#pragma unroll
-        for (int x = 0; x < K; x++) carry[x] = u32x4{0u, 0u, 0u, 0u};
-        auto u16at = [&](const uint8_t *row, int o) -> uint32_t {
-            return *reinterpret_cast<const uint16_t *>(row + (o < 0 ? 0 : o));
-        };
         for (uint32_t z = 0; z < (uint32_t)(kQ * kQ); z++) {
-            lds_barrier();                                    // B2: plane z's image is final
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // plane z + 1 landed (and the stores before it)
-            lds_barrier();                                    // B1: the compute waves are done with slot z
-            const uint8_t *slot8 = lds8 + (z & 1u) * kSlotBytes;
-#pragma unroll
-            for (int x = 0; x < K; x++) {
-                const uint8_t *row = slot8 + x * RW;
-                const uint32_t a = __builtin_amdgcn_readfirstlane(slice_off(x) + z * sc);  // row start (from J.dst)
-                const uint32_t am = (dst_mod + a) & 127u;                                 // its line offset
-                const uint32_t fl = a - am;                                               // floor128(start)
-                const uint32_t f = z == 0 ? fl + (am ? 128u : 0u) : fl;                   // line-part start
-                const uint32_t le = fl + ((am + sc) & ~127u);                             // floor128(end)
-                const uint32_t nbl = (le - f) >> 4;
-                // block b: absolute bytes [f + 16 b, +16), row offsets k .. k + 15 (k < 0: the carry)
-                auto block = [&](uint32_t b, bool use_carry) -> u32x4 {
-                    const int k = (int)(f + 16u * b) - (int)a;
-                    uint32_t h[8];
-#pragma unroll
-                    for (int i = 0; i < 8; i++) {
-                        const int o = k + 2 * i;
-                        const uint32_t cw = carry[x][i >> 1], ch = (i & 1) ? cw >> 16 : cw & 0xffffu;
-                        const uint32_t rv = u16at(row, o);
-                        h[i] = (use_carry && o < 0) ? ch : rv;
-                    }
-                    return u32x4{h[0] | h[1] << 16, h[2] | h[3] << 16, h[4] | h[5] << 16, h[6] | h[7] << 16};
-                };
-                const u32x4 q0 = block(lane, true), q1 = block(64u + lane, false);
-                // the row's tail line (blocks nbl .. nbl + 7, in q1) becomes the node's carry
-                const int src_lane = (int)(nbl - 64u) + (int)(lane & 7u);
-                carry[x].x = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)q1.x);
-                carry[x].y = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)q1.y);
-                carry[x].z = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)q1.z);
-                carry[x].w = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)q1.w);
-                if (!((store_mask >> x) & 1u)) continue;
-                if (z == 0) {  // the chunk's head: its first 128 bytes exactly (up to the first whole line)
-                    const u32x4 hv = *reinterpret_cast<const u32x4 *>(row + 16u * (lane & 7u));
-                    __builtin_amdgcn_raw_buffer_store_b128(hv, rb_dst, (int)(lane < 8u ? 16u * lane : kDrop), (int)a, kStAux);
-                }
-                if (z == (uint32_t)(kQ * kQ - 1)) {  // the chunk's tail: its last 128 bytes, exactly
-                    uint32_t h[8];
-#pragma unroll
-                    for (int i = 0; i < 8; i++) h[i] = u16at(row, (int)(sc - 128u + 16u * (lane & 7u)) + 2 * i);
-                    const u32x4 tv = {h[0] | h[1] << 16, h[2] | h[3] << 16, h[4] | h[5] << 16, h[6] | h[7] << 16};
-                    __builtin_amdgcn_raw_buffer_store_b128(tv, rb_dst, (int)(lane < 8u ? 16u * lane : kDrop),
-                                                           (int)(a + sc - 128u), kStAux);
-                }
-                __builtin_amdgcn_raw_buffer_store_b128(q0, rb_dst, (int)(lane < nbl ? 16u * lane : kDrop), (int)f, kStAux);
-                __builtin_amdgcn_raw_buffer_store_b128(q1, rb_dst, (int)(64u + lane < nbl ? 16u * (64u + lane) : kDrop),
-                                                       (int)f, kStAux);
-            }
-            // slot z is read: plane z + 2 may land there (the DMA is issued after the reads' data
-            // has been consumed by the stores above)
+            lds_barrier();                                  // B2
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // plane z + 1 landed
+            lds_barrier();                                  // B1
             if (z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, (z & 1u) * kSlotBytes);
         }
         return;
@@ -551,7 +465,7 @@ __global__ void __launch_bounds__(kWaves * 64, 4) enc_dma_kernel(EncArgs a) {
         }
     }
     // the last plane's left-over row (its staging row is untouched since the last compute)
-    if (!kSysLx && wv == 0) {
+    if (wv == 0) {
         const uint32_t it = kFlush.extra, src = it & 0xffu;
         const uint8_t *row = lds8 + kStageBase + src * RW;
         const u32x4 e0 = *reinterpret_cast<const u32x4 *>(row + lo0);

@@ -957,9 +957,7 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
             j.rot = rotated ? (uint32_t)((st * TE_ROTATION_STEP) % n) : 0u;
             j.dst_skew = (uint32_t)(st * cs);
             const bool masked = ((reinterpret_cast<uintptr_t>(j.src) & 3u) + j.src_len) % 4 != 0;
-            // odd source or slice bytes: the fast kernels read 2-aligned rows (and the LDS-DMA
-            // kernel's line-exact systematic stores read 2-aligned row offsets): generic kernel
-            const bool odd = ((reinterpret_cast<uintptr_t>(j.src) | reinterpret_cast<uintptr_t>(j.dst)) & 1u) != 0;
+            const bool odd = (reinterpret_cast<uintptr_t>(j.src) & 1u) != 0;
             groups[GeomKey{cs, slice_len, masked, odd}].push_back(j);
         }
         if (!raw && !keep) {
