@@ -302,6 +302,9 @@ __global__ void __launch_bounds__(kWaves * 64, 4) enc_dma_kernel(EncArgs a) {
 #pragma unroll
         for (int p = 0; p < 9; p++) {
             const uint32_t x = (uint32_t)p + ((uint32_t)p >= nz0 ? 1u : 0u);
+            // level 2 reads node z0's rows 7.. only for the pairs z0 finishes (x < z0): rows 8, 9 of
+            // row 7 and row 9 of row 8 are never used (30 of the stripe's 270 read-backs)
+            if (lvl2 && x >= (uint32_t)K && x > nz0) continue;
             piece(lvl2, TEC_DMA_ROWPOL == 1 && (lvl2 ? TEC_DMA_L2NT != 0 : x < nz0), so_pbase + x * kQ * sc,
                   slot + kPartBase + p * RW);
         }
