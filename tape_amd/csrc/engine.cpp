@@ -3774,12 +3774,23 @@ size_t te_outer_chunk_bytes(uint32_t k, size_t len) {  // outer.rs:74-80
     return (raw + 63) / 64 * 64;
 }
 
+}  // extern "C"
+namespace {
+int outer_encode_matrix(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t chunk_bytes, uint32_t segments,
+                        uint64_t seg_in, uint8_t *d_out, uint64_t seg_out, hipStream_t s);
+}
+extern "C" {
+
 int te_outer_encode_device(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t chunk_bytes, uint32_t segments,
                            uint64_t seg_in, uint8_t *d_out, uint64_t seg_out, void *stream) {
     if (k == 0 || m == 0 || !d_in || !d_out || chunk_bytes == 0 || chunk_bytes % 64 || chunk_bytes / 2 > 0xffffffffull)
         return TE_ERR_INVALID_ARG;
     if (rs16::use_high_rate(k, m) < 0) return TE_ERR_UNSUPPORTED;
     if (device_count() <= 0) return TE_ERR_NO_DEVICE;
+    // the encode as a matrix product (rs16_matrix_kernel) when its lookup image fits the LDS budget:
+    // OuterCoder(17, 50) 17 x 33; the transforms below otherwise
+    if (rs16_mat_supported(k, m) && !tec_knob("TEC_RS16_NO_MATRIX"))
+        return outer_encode_matrix(k, m, d_in, chunk_bytes, segments, seg_in, d_out, seg_out, (hipStream_t)stream);
     const rs16::Tables &T = rs16::tables();
     const uint32_t c = rs16::chunk(k, m), span = rs16::skew_span(k, m), wl = rs16::work_len(k, m);
     if ((size_t)span * 128 + (size_t)wl * 256 > 160 * 1024 || span > rs16::kModulus) return TE_ERR_UNSUPPORTED;
@@ -3849,6 +3860,7 @@ namespace {
 constexpr size_t kOuterLutCache = 64;
 struct OuterLut {
     uint16_t *d = nullptr;
+    bool mat = false;      // rs16::mat_image for rs16_matrix_kernel (else per-coefficient nibble tables)
     ReaderEvents readers;  // the last launches that read the table, per stream
     uint64_t tick = 0;
 };
@@ -3868,19 +3880,32 @@ int outer_lut(uint32_t k, uint32_t m, const std::vector<uint32_t> &recv, const s
         out = &it->second;
         return TE_OK;
     }
-    std::vector<uint16_t> D;
-    if (!rs16::decode_matrix(k, m, recv, D)) return TE_ERR_INVALID_LAYOUT;
-    const rs16::Tables &T = rs16::tables();
     const uint32_t nm = (uint32_t)miss.size();
-    std::vector<uint16_t> lut((size_t)nm * k * 64, 0);
-    for (uint32_t i = 0; i < nm; i++)
-        for (uint32_t r = 0; r < k; r++) {
-            const uint16_t coef = D[(size_t)miss[i] * k + r];
-            if (!coef) continue;
-            for (int q = 0; q < 4; q++)
-                for (uint32_t nb = 0; nb < 16; nb++)
-                    lut[((size_t)i * k + r) * 64 + q * 16 + nb] = T.gmul((uint16_t)(nb << (4 * q)), coef);
-        }
+    const bool enc = nm == 1 && miss[0] == 0xfffffffeu;  // the encode matrix (outer_enc_lut)
+    const uint32_t rows = enc ? m : nm;
+    std::vector<uint16_t> D;
+    if (enc) rs16::encode_matrix(k, m, D);
+    else if (!rs16::decode_matrix(k, m, recv, D)) return TE_ERR_INVALID_LAYOUT;
+    const bool mat = rs16_mat_supported(k, rows);
+    if (enc && !mat) return TE_ERR_UNSUPPORTED;
+    std::vector<uint16_t> lut;
+    if (mat) {  // the missing rows of D, as the matrix kernel's lookup image
+        std::vector<uint16_t> Dm((size_t)rows * k);
+        for (uint32_t i = 0; i < rows; i++)
+            memcpy(&Dm[(size_t)i * k], &D[(size_t)(enc ? i : miss[i]) * k], k * sizeof(uint16_t));
+        lut = rs16::mat_image(k, rows, Dm.data());
+    } else {
+        const rs16::Tables &T = rs16::tables();
+        lut.assign((size_t)nm * k * 64, 0);
+        for (uint32_t i = 0; i < nm; i++)
+            for (uint32_t r = 0; r < k; r++) {
+                const uint16_t coef = D[(size_t)miss[i] * k + r];
+                if (!coef) continue;
+                for (int q = 0; q < 4; q++)
+                    for (uint32_t nb = 0; nb < 16; nb++)
+                        lut[((size_t)i * k + r) * 64 + q * 16 + nb] = T.gmul((uint16_t)(nb << (4 * q)), coef);
+            }
+    }
     if (g_outer_luts.size() >= kOuterLutCache) {
         auto lru = g_outer_luts.begin();
         for (auto j = g_outer_luts.begin(); j != g_outer_luts.end(); ++j)
@@ -3897,9 +3922,63 @@ int outer_lut(uint32_t k, uint32_t m, const std::vector<uint32_t> &recv, const s
         (void)hipFree(L.d);
         return hip_status(e);
     }
+    L.mat = mat;
     L.tick = ++g_outer_tick;
     out = &(g_outer_luts[key] = L);
     return TE_OK;
+}
+
+// The encode matrix's image, cached like a decode pattern's (key: received = none, missing = the
+// marker 0xfffffffe); the launch waits for its stream (te_outer_encode_device's contract).
+int outer_encode_matrix(uint32_t k, uint32_t m, const uint8_t *d_in, uint64_t chunk_bytes, uint32_t segments,
+                        uint64_t seg_in, uint8_t *d_out, uint64_t seg_out, hipStream_t s) {
+    int dev = 0;
+    TE_HIP(hipGetDevice(&dev));
+    int r = TE_OK;
+    {
+        std::lock_guard<std::mutex> lk(g_outer_mu);
+        OuterLut *L = nullptr;
+        if ((r = outer_lut(k, m, {}, {0xfffffffeu}, dev, L))) return r;
+        Rs16MatArgs a{};
+        a.in = d_in;
+        a.out = d_out;
+        a.in_stride = a.out_stride = chunk_bytes;
+        a.seg_in = seg_in;
+        a.seg_out = seg_out;
+        a.tab = L->d;
+        a.k = k; a.rows = m; a.elems = (uint32_t)(chunk_bytes / 2); a.segments = segments; a.ptrs = 0;
+        KTimer kt(s);
+        r = hip_status(launch_rs16_matrix(a, s));
+        kt.stop();
+        if (r == TE_OK) r = hip_status(L->readers.record(s));
+    }
+    if (r == TE_OK) r = hip_status(hipStreamSynchronize(s));
+    return r;
+}
+
+// Restore a group's missing chunks: `cnt` segments whose shard pointers are laid out as
+// Rs16DecArgs::ptr (per segment k received, then nm outputs), through the matrix kernel when the
+// pattern's table is a matrix image.
+int outer_restore(const OuterLut *L, uint32_t k, uint32_t nm, const uint8_t *const *ptr, uint32_t cnt,
+                  uint64_t chunk_bytes, hipStream_t s) {
+    if (L->mat) {
+        Rs16MatArgs a{};
+        memcpy(a.ptr, ptr, (size_t)cnt * (k + nm) * sizeof(ptr[0]));
+        a.tab = L->d;
+        a.k = k; a.rows = nm; a.elems = (uint32_t)(chunk_bytes / 2); a.segments = cnt; a.ptrs = 1;
+        KTimer kt(s);
+        const int r = hip_status(launch_rs16_matrix(a, s));
+        kt.stop();
+        return r;
+    }
+    Rs16DecArgs a{};
+    memcpy(a.ptr, ptr, (size_t)cnt * (k + nm) * sizeof(ptr[0]));
+    a.lut = L->d;
+    a.k = k; a.nmiss = nm; a.elems = (uint32_t)(chunk_bytes / 2);
+    KTimer kt(s);
+    const int r = hip_status(launch_rs16_decode(a, cnt, s));
+    kt.stop();
+    return r;
 }
 }  // namespace
 
@@ -3935,18 +4014,14 @@ int te_outer_decode(uint32_t k, uint32_t n, const uint8_t *const *chunks, size_t
     const size_t sh = (size_t)k * chunk_bytes, rs = (size_t)nm * chunk_bytes;
     uint8_t *d = nullptr;
     TE_HIP(hipMalloc((void **)&d, sh + rs));
-    Rs16DecArgs a{};
+    std::vector<const uint8_t *> ptr(k + nm);
     for (uint32_t j = 0; j < k && r == TE_OK; j++) {
-        a.ptr[j] = d + (size_t)j * chunk_bytes;
+        ptr[j] = d + (size_t)j * chunk_bytes;
         r = hip_status(hipMemcpy(d + (size_t)j * chunk_bytes, chunks[recv[j]], chunk_bytes, hipMemcpyHostToDevice));
     }
-    for (uint32_t i = 0; i < nm; i++) a.ptr[k + i] = d + sh + (size_t)i * chunk_bytes;
+    for (uint32_t i = 0; i < nm; i++) ptr[k + i] = d + sh + (size_t)i * chunk_bytes;
     if (r == TE_OK) {
-        a.lut = L->d;
-        a.k = k; a.nmiss = nm; a.elems = (uint32_t)(chunk_bytes / 2);
-        KTimer kt(nullptr);
-        r = hip_status(launch_rs16_decode(a, 1, nullptr));
-        kt.stop();
+        r = outer_restore(L, k, nm, ptr.data(), 1, chunk_bytes, nullptr);
         if (r == TE_OK) r = hip_status(L->readers.record(nullptr));
     }
     for (uint32_t i = 0; i < nm && r == TE_OK; i++)
@@ -4009,18 +4084,13 @@ int outer_decode_segs(uint32_t k, uint32_t n, const uint8_t *const *d_chunks, ui
         if ((r = outer_lut(k, m, recv, miss, dev, L))) return r;
         for (size_t g0 = 0; g0 < gr.second.size(); g0 += fit) {
             const uint32_t cnt = (uint32_t)std::min<size_t>(fit, gr.second.size() - g0);
-            Rs16DecArgs a{};
+            const uint8_t *ptr[kRs16DecPtrs];
             for (uint32_t q = 0; q < cnt; q++) {
                 const uint32_t g = gr.second[g0 + q];
-                for (uint32_t j = 0; j < k; j++) a.ptr[q * per + j] = d_chunks[(size_t)g * n + recv[j]];
-                for (uint32_t i = 0; i < nm; i++) a.ptr[q * per + k + i] = d_out + g * seg_out + (size_t)miss[i] * chunk_bytes;
+                for (uint32_t j = 0; j < k; j++) ptr[q * per + j] = d_chunks[(size_t)g * n + recv[j]];
+                for (uint32_t i = 0; i < nm; i++) ptr[q * per + k + i] = d_out + g * seg_out + (size_t)miss[i] * chunk_bytes;
             }
-            a.lut = L->d;
-            a.k = k; a.nmiss = nm; a.elems = (uint32_t)(chunk_bytes / 2);
-            KTimer kt(s);
-            r = hip_status(launch_rs16_decode(a, cnt, s));
-            kt.stop();
-            if (r) return r;
+            if ((r = outer_restore(L, k, nm, ptr, cnt, chunk_bytes, s))) return r;
         }
         if ((r = hip_status(L->readers.record(s)))) return r;
     }

@@ -275,6 +275,27 @@ struct Rs16DecArgs {
     const uint16_t *lut;            // nmiss x k nibble tables (decoding-matrix coefficients)
     uint32_t k, nmiss, elems;
 };
+// GF(2^16) matrix apply (rs16.hip rs16_matrix_kernel), the encode and the decode both:
+// out[i] = sum_r M[i][r] * in[r] for i < rows, r < k.  `tab` is M's packed lookup image
+// (rs16::mat_image): per input r, nibble q and group g of 4 rows, 16 entries of 4 u16 -- entry n
+// holds M[4g + j][r] * (n << 4q) for j = 0..3 -- so one 8-byte LDS read serves 4 rows' products.
+constexpr uint32_t kRs16MatMaxG = 16;          // rows <= 64
+constexpr uint32_t kRs16MatLds = 80 * 1024;    // image bytes (k * G * 512) staged per block: 2 blocks per CU
+struct Rs16MatArgs {
+    const uint8_t *in;   // ptrs == 0: input r of segment g at in + g * seg_in + r * in_stride,
+    uint8_t *out;        //            output i at out + g * seg_out + i * out_stride
+    uint64_t in_stride, out_stride, seg_in, seg_out;
+    const uint8_t *ptr[kRs16DecPtrs];  // ptrs == 1: segment g's k inputs then rows outputs at ptr[g * (k + rows) + j]
+    const uint16_t *tab;
+    uint32_t k, rows, elems, segments, ptrs;
+    uint32_t rstride;  // set by the launcher: image bytes per input (a run-time value, so the kernel's
+                       // per-input bases stay one scalar each instead of 4k folded constants)
+};
+inline size_t rs16_mat_bytes(uint32_t k, uint32_t rows) { return (size_t)k * ((rows + 3) / 4) * 512u; }
+inline bool rs16_mat_supported(uint32_t k, uint32_t rows) {
+    return k >= 1 && k <= 32 && rows >= 1 && (rows + 3) / 4 <= kRs16MatMaxG && rs16_mat_bytes(k, rows) <= kRs16MatLds;
+}
+hipError_t launch_rs16_matrix(const Rs16MatArgs &a, hipStream_t s);
 hipError_t launch_rs16_encode(const Rs16EncArgs &a, uint32_t segments, hipStream_t s);
 hipError_t launch_rs16_decode(const Rs16DecArgs &a, uint32_t segments, hipStream_t s);
 hipError_t launch_repair(const RepArgs &a, uint32_t max_erased, hipStream_t s);

@@ -17,6 +17,9 @@ namespace tec {
 namespace rs16k {
 
 constexpr uint32_t kRs16DecLds = 48 * 1024;  // decoding tables staged in LDS up to this size
+#ifndef TEC_RS16_REG
+#define TEC_RS16_REG 1  // low rate, chunk <= 32: rs16_encode_low_kernel (work vector in VGPRs)
+#endif
 #ifndef TEC_RS16_UNROLL
 #define TEC_RS16_UNROLL 1  // butterfly groups in flight per thread in the transforms' inner loops
 #endif
@@ -174,6 +177,289 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(TEC_R
     for (uint32_t j = 0; j < m; j++) st_elem(a.out + (uint64_t)j * a.out_stride, e, c.ld(j));
 }
 
+// ---- low rate, chunk C <= 32: the work vector in registers ----
+// The kernel above keeps a thread's work vector in LDS, so every butterfly group adds 4 loads and 4
+// stores to the 4 table lookups of each product: 6 LDS accesses per product on a kernel whose
+// bound is the LDS pipe (r04/r05: OuterCoder(17, 50) at 3.94 ms, 0.107 of HBM).  With C fixed at
+// compile time the transforms unroll completely, every work index is a constant and the vector
+// lives in VGPRs (C values + C kept IFFT values); a product is then its 4 conflict-free lookups
+// (one multiplier's 16-entry nibble table is 8 dwords in 8 banks).  The truncation tests (r <
+// trunc) and the chunk offsets are uniform branches on kernel arguments.
+// Tables are addressed by LDS byte offset (uint32_t) rather than through the extern array, so a
+// lookup is a bit-field extract plus one shift-add of the multiplier's (uniform) table offset.
+typedef __attribute__((address_space(3))) const uint16_t lds_u16;
+__device__ __forceinline__ uint32_t lds_ld16(uint32_t a) { return *reinterpret_cast<lds_u16 *>((size_t)a); }
+// v_bfe_u32 by hand: the compiler rewrites a field extract followed by << 1 as a shift and a mask
+// (3 VALU per lookup with the add); extract + v_lshl_add_u32 is 2
+__device__ __forceinline__ uint32_t nib(uint32_t x, int q) {
+    uint32_t n;
+    asm("v_bfe_u32 %0, %1, %2, 4" : "=v"(n) : "v"(x), "i"(4 * q));
+    return n;
+}
+__device__ __forceinline__ uint32_t mulx_a(uint32_t x, uint32_t tb) {  // tb: the table's byte offset
+    const uint32_t t0 = lds_ld16((nib(x, 0) << 1) + tb);
+    const uint32_t t1 = lds_ld16((nib(x, 1) << 1) + (tb + 32u));
+    const uint32_t t2 = lds_ld16((nib(x, 2) << 1) + (tb + 64u));
+    const uint32_t t3 = lds_ld16((nib(x, 3) << 1) + (tb + 96u));
+    return t0 ^ t1 ^ t2 ^ t3;
+}
+
+template <int DIST, int DIST4, int C>
+__device__ __forceinline__ void ifft_layer_r(uint32_t (&w)[C], uint32_t lut, uint32_t trunc, uint32_t delta) {
+#pragma unroll
+    for (int r = 0; r < C; r += DIST4) {
+        if ((uint32_t)r >= trunc) continue;  // (not break: a run-time exit leaves the loop rolled)
+        const uint32_t b = r + DIST + delta - 1;
+        const uint32_t t0 = lut + b * 128u, t1 = t0 + DIST * 128u, t2 = t0 + 2 * DIST * 128u;
+#pragma unroll
+        for (int i = r; i < r + DIST; i++) {
+            uint32_t &x0 = w[i], &x1 = w[i + DIST], &x2 = w[i + 2 * DIST], &x3 = w[i + 3 * DIST];
+            x1 ^= x0;
+            x0 ^= mulx_a(x1, t0);
+            x3 ^= x2;
+            x2 ^= mulx_a(x3, t2);
+            x2 ^= x0;
+            x0 ^= mulx_a(x2, t1);
+            x3 ^= x1;
+            x1 ^= mulx_a(x3, t1);
+        }
+    }
+}
+template <int DIST, int C>
+__device__ __forceinline__ void ifft_r(uint32_t (&w)[C], uint32_t lut, uint32_t trunc, uint32_t delta) {
+    if constexpr (DIST * 4 <= C) {
+        ifft_layer_r<DIST, DIST * 4, C>(w, lut, trunc, delta);
+        ifft_r<DIST * 4, C>(w, lut, trunc, delta);
+    } else if constexpr (DIST < C) {
+        const uint32_t t = lut + (DIST + delta - 1) * 128u;
+#pragma unroll
+        for (int i = 0; i < DIST; i++) {
+            w[i + DIST] ^= w[i];
+            w[i] ^= mulx_a(w[i + DIST], t);
+        }
+    }
+}
+template <int DIST4, int C>
+__device__ __forceinline__ void fft_r(uint32_t (&w)[C], uint32_t lut, uint32_t trunc, uint32_t delta) {
+    constexpr int DIST = DIST4 / 4;
+    if constexpr (DIST >= 1) {
+#pragma unroll
+        for (int r = 0; r < C; r += DIST4) {
+            if ((uint32_t)r >= trunc) continue;
+            const uint32_t b = r + DIST + delta - 1;
+            const uint32_t t0 = lut + b * 128u, t1 = t0 + DIST * 128u, t2 = t0 + 2 * DIST * 128u;
+#pragma unroll
+            for (int i = r; i < r + DIST; i++) {
+                uint32_t &x0 = w[i], &x1 = w[i + DIST], &x2 = w[i + 2 * DIST], &x3 = w[i + 3 * DIST];
+                x0 ^= mulx_a(x2, t1);
+                x2 ^= x0;
+                x1 ^= mulx_a(x3, t1);
+                x3 ^= x1;
+                x0 ^= mulx_a(x1, t0);
+                x1 ^= x0;
+                x2 ^= mulx_a(x3, t2);
+                x3 ^= x2;
+            }
+        }
+        fft_r<DIST, C>(w, lut, trunc, delta);
+    } else if constexpr (DIST4 == 2) {
+#pragma unroll
+        for (int r = 0; r < C; r += 2) {
+            if ((uint32_t)r >= trunc) continue;
+            w[r] ^= mulx_a(w[r + 1], lut + (r + delta) * 128u);
+            w[r + 1] ^= w[r];
+        }
+    }
+}
+
+#ifndef TEC_RS16_LOW_WPE
+#define TEC_RS16_LOW_WPE 4
+#endif
+template <int C>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TEC_RS16_LOW_WPE)))
+rs16_encode_low_kernel(Rs16EncArgs a) {  // grid.y = segments
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds16[];
+    for (uint32_t t = threadIdx.x; t < a.span * 32u; t += blockDim.x)
+        reinterpret_cast<uint32_t *>(lds16)[t] = reinterpret_cast<const uint32_t *>(a.lut)[t];
+    __syncthreads();
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= a.elems) return;  // no barrier below
+    const uint32_t lut = (uint32_t)(size_t)(lds_u16 *)lds16;
+    const uint8_t *in = a.in + (uint64_t)blockIdx.y * a.seg_in;
+    uint8_t *out = a.out + (uint64_t)blockIdx.y * a.seg_out;
+    const uint32_t k = a.k, m = a.m;
+    uint32_t w[C], keep[C];
+    // every load issued before the first use: the shards past k re-read shard k - 1 (same lines,
+    // cache hits) and are zeroed after, instead of a branch and a wait per shard
+#pragma unroll
+    for (int j = 0; j < C; j++) w[j] = ld_elem(in + (uint64_t)((uint32_t)j < k ? (uint32_t)j : k - 1u) * a.in_stride, e);
+#pragma unroll
+    for (int j = 0; j < C; j++) w[j] = (uint32_t)j < k ? w[j] : 0u;
+    ifft_r<1, C>(w, lut, k, 0);
+#pragma unroll
+    for (int j = 0; j < C; j++) keep[j] = w[j];
+#pragma unroll 1
+    for (uint32_t s = 0; s < m; s += C) {
+        if (s) {
+#pragma unroll
+            for (int j = 0; j < C; j++) w[j] = keep[j];
+        }
+        const uint32_t n = m - s < (uint32_t)C ? m - s : (uint32_t)C;
+        fft_r<C, C>(w, lut, n, s + C);
+#pragma unroll
+        for (int j = 0; j < C; j++)
+            if ((uint32_t)j < n) st_elem(out + (uint64_t)(s + j) * a.out_stride, e, w[j]);
+    }
+}
+
+// ---- matrix apply: out[i] = sum_r M[i][r] * in[r] (encode: M = the encode matrix; decode: the
+// decoding matrix's missing rows) ----
+// The FFT encode's products each have their own multiplier and input, so each costs 4 ds_read_u16
+// (2 LDS cycles each) and ~14 VALU.  As a matrix the products of one input share their nibble
+// indices across every output row: the image packs 4 rows' table entries into 8 bytes, so one
+// ds_read_b64 (2 cycles, conflict-free: a 16-entry x 8 B table is 32 dwords in distinct banks)
+// serves 4 products, and the nibble extraction is paid once per input instead of once per
+// product.  OuterCoder(17, 50): 17 x 36 products per column (vs ~190 in the transforms) at 0.5
+// LDS cycles and ~1.3 VALU each.  A thread owns two adjacent elements (their low bytes adjacent:
+// 16-bit loads and stores); the image is staged once per block and the blocks loop over the
+// (segment, column-tile) space.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const u32x2 lds_u32x2;
+typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
+
+// One input's products: the image block of (r, q) holds G / 2 pairs of row groups as 16-entry
+// tables of 16 B (8 rows per ds_read_b128: 4 LDS cycles, conflict-free -- 16 distinct entries
+// fill the 64 banks once) and, for odd G, the last group as a 16-entry table of 8 B
+// (ds_read_b64).  Not 8-byte reads throughout: the compiler pairs those into ds_read2_b64, which
+// costs 8 cycles for the two instead of 4.  The four nibble tables' entries of a group are XORed
+// together before the accumulator (bitop3: 2 VALU per dword).
+// three-input XOR (v_bitop3_b32 0x96): the compiler leaves XOR chains as 2-input v_xor_b32
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
+template <int G>
+__device__ __forceinline__ void mat_input(uint32_t (&acc0)[2 * G], uint32_t (&acc1)[2 * G], const uint8_t *blk,
+                                          uint32_t x01) {  // blk: input r's image (4 x G x 128 B); x01: element 0 | element 1 << 16
+    constexpr int NP = G / 2;
+    uint32_t n0[4], n1[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        n0[q] = nib(x01, q);
+        n1[q] = nib(x01, q + 4);
+    }
+#pragma unroll
+    for (int h = 0; h < NP; h++) {
+        u32x4 v0[4], v1[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            v0[q] = *(lds_u32x4 *)(blk + (n0[q] << 4) + (q * G * 128 + h * 256));
+            v1[q] = *(lds_u32x4 *)(blk + (n1[q] << 4) + (q * G * 128 + h * 256));
+        }
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            acc0[4 * h + d] = xor3(xor3(acc0[4 * h + d], v0[0][d], v0[1][d]), v0[2][d], v0[3][d]);
+            acc1[4 * h + d] = xor3(xor3(acc1[4 * h + d], v1[0][d], v1[1][d]), v1[2][d], v1[3][d]);
+        }
+    }
+    if constexpr (G % 2) {  // tail group: entries of 8 B at NP * 256 within each nibble block
+        u32x2 v0[4], v1[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            v0[q] = *(lds_u32x2 *)(blk + (n0[q] << 3) + (q * G * 128 + NP * 256));
+            v1[q] = *(lds_u32x2 *)(blk + (n1[q] << 3) + (q * G * 128 + NP * 256));
+        }
+#pragma unroll
+        for (int d = 0; d < 2; d++) {
+            acc0[4 * NP + d] = xor3(xor3(acc0[4 * NP + d], v0[0][d], v0[1][d]), v0[2][d], v0[3][d]);
+            acc1[4 * NP + d] = xor3(xor3(acc1[4 * NP + d], v1[0][d], v1[1][d]), v1[2][d], v1[3][d]);
+        }
+    }
+}
+
+template <int G, int KB, bool PTRS>  // KB: input slots (k <= KB)
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) rs16_matrix_kernel(Rs16MatArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds16[];
+    {
+        const uint32_t n16 = a.k * (uint32_t)G * 32u;  // 16-byte units of the image
+        for (uint32_t t = threadIdx.x; t < n16; t += blockDim.x)
+            reinterpret_cast<uint4 *>(lds16)[t] = reinterpret_cast<const uint4 *>(a.tab)[t];
+    }
+    __syncthreads();
+    const uint8_t *tab = reinterpret_cast<const uint8_t *>(lds16);
+    const uint32_t pairs = a.elems >> 1, tps = (pairs + blockDim.x - 1) / blockDim.x;
+    const uint32_t ntiles = a.segments * tps;
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {  // no barrier in the loop
+        // k and the strides re-read opaquely per tile: loop-invariant, the per-input and per-row
+        // offsets derived from them were hoisted out of the tile loop (~100 scalars, 324 SGPRs
+        // spilled to VGPR lanes); a few scalar ops per tile instead
+        uint32_t k = a.k, rstride = a.rstride;
+        uint64_t in_stride = a.in_stride, out_stride = a.out_stride;
+        asm volatile("" : "+s"(k), "+s"(rstride), "+s"(in_stride), "+s"(out_stride));
+        const uint32_t seg = tile / tps, p = (tile - seg * tps) * blockDim.x + threadIdx.x;
+        if (p >= pairs) continue;
+        const uint32_t e0 = 2u * p, eo = (e0 >> 5) * 64u + (e0 & 31u);
+        auto inp = [&](uint32_t r) -> const uint8_t * {
+            if constexpr (PTRS) return a.ptr[seg * (k + a.rows) + r] + eo;
+            else return a.in + (uint64_t)seg * a.seg_in + (uint64_t)r * in_stride + eo;
+        };
+        uint32_t acc0[2 * G], acc1[2 * G];
+#pragma unroll
+        for (int i = 0; i < 2 * G; i++) acc0[i] = acc1[i] = 0;
+        // every input's two 16-bit words loaded up front (KB >= k slots, indices past k - 1 clamped),
+        // both elements packed into one VGPR (x0 | x1 << 16, one v_perm), and all of them pinned
+        // here by an empty asm: otherwise the compiler sinks each load into the run-time-guarded
+        // block that uses it and waits for it there, one HBM latency per input (a rolling prefetch
+        // in a loop fared no better: its waits came out as vmcnt(0)).  One wait per tile; the
+        // other waves on the CU cover it.
+        uint32_t P[KB];
+#pragma unroll
+        for (int j = 0; j < KB; j++) {
+            const uint8_t *s = inp((uint32_t)j < k ? (uint32_t)j : k - 1u);
+            const uint32_t lo = *reinterpret_cast<const uint16_t *>(s), hi = *reinterpret_cast<const uint16_t *>(s + 32);
+            P[j] = __builtin_amdgcn_perm(hi, lo, 0x05010400u);  // [lo.b0, hi.b0, lo.b1, hi.b1]
+        }
+#pragma unroll
+        for (int j = 0; j < KB; j++) asm volatile("" ::"v"(P[j]));
+#pragma unroll
+        for (int r = 0; r < KB; r++)
+            if ((uint32_t)r < k) mat_input<G>(acc0, acc1, tab + r * rstride, P[r]);
+#pragma unroll
+        for (int i = 0; i < 4 * G; i++) {
+            if ((uint32_t)i >= a.rows) continue;
+            const uint32_t v0 = (acc0[i >> 1] >> (16 * (i & 1))) & 0xffffu, v1 = (acc1[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+            uint8_t *o;
+            if constexpr (PTRS) o = const_cast<uint8_t *>(a.ptr[seg * (k + a.rows) + k + i]) + eo;
+            else o = a.out + (uint64_t)seg * a.seg_out + (uint64_t)i * out_stride + eo;
+            *reinterpret_cast<uint16_t *>(o) = (uint16_t)((v0 & 0xffu) | (v1 & 0xffu) << 8);
+            *reinterpret_cast<uint16_t *>(o + 32) = (uint16_t)((v0 >> 8) | (v1 & 0xff00u));
+        }
+    }
+}
+
+template <int G, int KB>
+hipError_t launch_mat_gk(Rs16MatArgs a, uint32_t grid, size_t lds, hipStream_t s) {
+    a.rstride = 4u * G * 128u;
+    const void *fn = a.ptrs ? reinterpret_cast<const void *>(rs16_matrix_kernel<G, KB, true>)
+                            : reinterpret_cast<const void *>(rs16_matrix_kernel<G, KB, false>);
+    if (const hipError_t e = ensure_dyn_lds(fn, lds); e != hipSuccess) return e;
+    if (a.ptrs) hipLaunchKernelGGL((rs16_matrix_kernel<G, KB, true>), dim3(grid), dim3(512), lds, s, a);
+    else hipLaunchKernelGGL((rs16_matrix_kernel<G, KB, false>), dim3(grid), dim3(512), lds, s, a);
+    return hipGetLastError();
+}
+template <int G>
+hipError_t launch_mat_g(const Rs16MatArgs &a, uint32_t grid, size_t lds, hipStream_t s) {
+    if constexpr (G <= (int)kRs16MatMaxG) {
+        if ((a.rows + 3) / 4 > (uint32_t)G) return launch_mat_g<G + 1>(a, grid, lds, s);
+        if (a.k <= 16) return launch_mat_gk<G, 16>(a, grid, lds, s);
+        if (a.k <= 32) return launch_mat_gk<G, 32>(a, grid, lds, s);
+    }
+    return hipErrorInvalidValue;
+}
+
 // Restore the missing originals: out[i] = sum_r D[i][r] * received[r] (nibble tables per
 // coefficient, staged in LDS).  REG (k <= 32): a thread loads its element of each received shard
 // once into registers and computes every missing output from them (the first kernel re-read the
@@ -294,6 +580,34 @@ static uint32_t rs16_enc_threads(const Rs16EncArgs &a, size_t *lds_out) {
 
 hipError_t launch_rs16_encode(const Rs16EncArgs &a, uint32_t segments, hipStream_t s) {
     if (a.elems == 0 || segments == 0) return hipSuccess;
+#if TEC_RS16_REG
+    if (a.one_chunk && a.c >= 1 && a.c <= 32) {
+        if (segments > 65535) return hipErrorInvalidValue;
+        const size_t lds = (size_t)a.span * 128u;
+        const dim3 grid((a.elems + 255) / 256, segments);
+        const void *fn = nullptr;
+        switch (a.c) {
+        case 1: fn = reinterpret_cast<const void *>(rs16k::rs16_encode_low_kernel<1>); break;
+        case 2: fn = reinterpret_cast<const void *>(rs16k::rs16_encode_low_kernel<2>); break;
+        case 4: fn = reinterpret_cast<const void *>(rs16k::rs16_encode_low_kernel<4>); break;
+        case 8: fn = reinterpret_cast<const void *>(rs16k::rs16_encode_low_kernel<8>); break;
+        case 16: fn = reinterpret_cast<const void *>(rs16k::rs16_encode_low_kernel<16>); break;
+        case 32: fn = reinterpret_cast<const void *>(rs16k::rs16_encode_low_kernel<32>); break;
+        default: return hipErrorInvalidValue;
+        }
+        const hipError_t e = ensure_dyn_lds(fn, lds);
+        if (e != hipSuccess) return e;
+        switch (a.c) {
+        case 1: hipLaunchKernelGGL(rs16k::rs16_encode_low_kernel<1>, grid, dim3(256), lds, s, a); break;
+        case 2: hipLaunchKernelGGL(rs16k::rs16_encode_low_kernel<2>, grid, dim3(256), lds, s, a); break;
+        case 4: hipLaunchKernelGGL(rs16k::rs16_encode_low_kernel<4>, grid, dim3(256), lds, s, a); break;
+        case 8: hipLaunchKernelGGL(rs16k::rs16_encode_low_kernel<8>, grid, dim3(256), lds, s, a); break;
+        case 16: hipLaunchKernelGGL(rs16k::rs16_encode_low_kernel<16>, grid, dim3(256), lds, s, a); break;
+        default: hipLaunchKernelGGL(rs16k::rs16_encode_low_kernel<32>, grid, dim3(256), lds, s, a); break;
+        }
+        return hipGetLastError();
+    }
+#endif
     size_t lds = 0;
     const uint32_t t = rs16_enc_threads(a, &lds);
     if (!t || segments > 65535) return hipErrorInvalidValue;
@@ -301,6 +615,18 @@ hipError_t launch_rs16_encode(const Rs16EncArgs &a, uint32_t segments, hipStream
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rs16k::rs16_encode_kernel, dim3((uint32_t)((a.elems + t - 1) / t), segments), dim3(t), lds, s, a);
     return hipGetLastError();
+}
+
+hipError_t launch_rs16_matrix(const Rs16MatArgs &a, hipStream_t s) {
+    if (a.elems == 0 || a.segments == 0) return hipSuccess;
+    if (!rs16_mat_supported(a.k, a.rows) || a.elems % 2) return hipErrorInvalidValue;
+    if (a.ptrs && (uint64_t)a.segments * (a.k + a.rows) > kRs16DecPtrs) return hipErrorInvalidValue;
+    const uint64_t tiles = (uint64_t)a.segments * (((a.elems >> 1) + 511) / 512);
+    if (tiles > 0xffffffffull) return hipErrorInvalidValue;
+    // a resident grid (2 blocks per CU at the largest image) looping over the tiles: the image is
+    // staged once per block, not once per 1,024 columns
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, 2048);
+    return rs16k::launch_mat_g<1>(a, grid, rs16_mat_bytes(a.k, a.rows), s);
 }
 
 hipError_t launch_rs16_decode(const Rs16DecArgs &a, uint32_t segments, hipStream_t s) {

@@ -198,5 +198,42 @@ inline bool decode_matrix(uint32_t k, uint32_t m, const std::vector<uint32_t> &r
     return true;
 }
 
+// The encode as a matrix: recovery j = sum_i E[j*k + i] * original i.  The transforms are linear
+// over GF(2^16) (every step is x ^= y * const), so column i is the encode of the unit vector e_i.
+inline void encode_matrix(uint32_t k, uint32_t m, std::vector<uint16_t> &E) {
+    std::vector<uint16_t> o(k), r(m);
+    E.assign((size_t)m * k, 0);
+    for (uint32_t i = 0; i < k; i++) {
+        std::fill(o.begin(), o.end(), 0);
+        o[i] = 1;
+        encode_column(k, m, o.data(), r.data());
+        for (uint32_t j = 0; j < m; j++) E[(size_t)j * k + i] = r[j];
+    }
+}
+
+// Lookup image of a rows x k matrix M for rs16_matrix_kernel (kernels.hpp Rs16MatArgs), G = the
+// 4-row groups: per input r and nibble position q a block of G x 64 u16 holding, for n < 16, the
+// products M[row][r] * (n << 4q) -- groups 2h and 2h + 1 (8 rows) as 16 entries of 8 u16 at h * 128
+// + n * 8, and for odd G the last group as 16 entries of 4 u16 at (G / 2) * 128 + n * 4.  Zero past
+// the last row.
+inline std::vector<uint16_t> mat_image(uint32_t k, uint32_t rows, const uint16_t *M) {
+    const Tables &T = tables();
+    const uint32_t G = (rows + 3) / 4, NP = G / 2;
+    std::vector<uint16_t> img((size_t)k * 4 * G * 64, 0);
+    for (uint32_t r = 0; r < k; r++)
+        for (uint32_t q = 0; q < 4; q++) {
+            uint16_t *blk = img.data() + ((size_t)r * 4 + q) * G * 64;
+            for (uint32_t row = 0; row < rows; row++) {
+                const uint32_t g = row / 4, j = row % 4;
+                const uint16_t c = M[(size_t)row * k + r];
+                for (uint32_t n = 0; n < 16; n++) {
+                    const size_t at = g < 2 * NP ? (g / 2) * 128 + n * 8 + (g % 2) * 4 + j : NP * 128 + n * 4 + j;
+                    blk[at] = T.gmul((uint16_t)(n << (4 * q)), c);
+                }
+            }
+        }
+    return img;
+}
+
 }  // namespace rs16
 }  // namespace tec
