@@ -341,47 +341,57 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return d;
 }
 
-template <int G>
-__device__ __forceinline__ void mat_input(uint32_t (&acc0)[2 * G], uint32_t (&acc1)[2 * G], const uint8_t *blk,
-                                          uint32_t x01) {  // blk: input r's image (4 x G x 128 B); x01: element 0 | element 1 << 16
+// One input's products for the thread's E elements (element e's 16 bits at bit sh + 16 e of w).
+template <int G, int E>
+__device__ __forceinline__ void mat_input(uint32_t (&acc)[E][2 * G], const uint8_t *blk, uint32_t w, int sh) {
     constexpr int NP = G / 2;
-    uint32_t n0[4], n1[4];
+    uint32_t n[E][4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        n0[q] = nib(x01, q);
-        n1[q] = nib(x01, q + 4);
-    }
+    for (int e = 0; e < E; e++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) n[e][q] = nib(w, (sh + 16 * e) / 4 + q);
 #pragma unroll
     for (int h = 0; h < NP; h++) {
-        u32x4 v0[4], v1[4];
+        u32x4 v[E][4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            v0[q] = *(lds_u32x4 *)(blk + (n0[q] << 4) + (q * G * 128 + h * 256));
-            v1[q] = *(lds_u32x4 *)(blk + (n1[q] << 4) + (q * G * 128 + h * 256));
-        }
+        for (int e = 0; e < E; e++)
 #pragma unroll
-        for (int d = 0; d < 4; d++) {
-            acc0[4 * h + d] = xor3(xor3(acc0[4 * h + d], v0[0][d], v0[1][d]), v0[2][d], v0[3][d]);
-            acc1[4 * h + d] = xor3(xor3(acc1[4 * h + d], v1[0][d], v1[1][d]), v1[2][d], v1[3][d]);
-        }
+            for (int q = 0; q < 4; q++) v[e][q] = *(lds_u32x4 *)(blk + (n[e][q] << 4) + (q * G * 128 + h * 256));
+#pragma unroll
+        for (int e = 0; e < E; e++)
+#pragma unroll
+            for (int d = 0; d < 4; d++)
+                acc[e][4 * h + d] = xor3(xor3(acc[e][4 * h + d], v[e][0][d], v[e][1][d]), v[e][2][d], v[e][3][d]);
     }
     if constexpr (G % 2) {  // tail group: entries of 8 B at NP * 256 within each nibble block
-        u32x2 v0[4], v1[4];
+        u32x2 v[E][4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            v0[q] = *(lds_u32x2 *)(blk + (n0[q] << 3) + (q * G * 128 + NP * 256));
-            v1[q] = *(lds_u32x2 *)(blk + (n1[q] << 3) + (q * G * 128 + NP * 256));
-        }
+        for (int e = 0; e < E; e++)
 #pragma unroll
-        for (int d = 0; d < 2; d++) {
-            acc0[4 * NP + d] = xor3(xor3(acc0[4 * NP + d], v0[0][d], v0[1][d]), v0[2][d], v0[3][d]);
-            acc1[4 * NP + d] = xor3(xor3(acc1[4 * NP + d], v1[0][d], v1[1][d]), v1[2][d], v1[3][d]);
-        }
+            for (int q = 0; q < 4; q++) v[e][q] = *(lds_u32x2 *)(blk + (n[e][q] << 3) + (q * G * 128 + NP * 256));
+#pragma unroll
+        for (int e = 0; e < E; e++)
+#pragma unroll
+            for (int d = 0; d < 2; d++)
+                acc[e][4 * NP + d] = xor3(xor3(acc[e][4 * NP + d], v[e][0][d], v[e][1][d]), v[e][2][d], v[e][3][d]);
     }
 }
 
+#ifndef TEC_RS16_MAT_E
+#define TEC_RS16_MAT_E 2     // elements per thread: 2 (16-bit loads / stores) or 1 (byte ones, fewer VGPRs)
+#endif
+#ifndef TEC_RS16_MAT_BT
+#define TEC_RS16_MAT_BT 512  // threads per block (2 blocks per CU at OuterCoder(17, 50)'s 78 KB image)
+#endif
+#ifndef TEC_RS16_MAT_WPE
+#define TEC_RS16_MAT_WPE 4   // waves per SIMD the registers are budgeted for
+#endif
+constexpr int kMatE = TEC_RS16_MAT_E, kMatBT = TEC_RS16_MAT_BT;
+
 template <int G, int KB, bool PTRS>  // KB: input slots (k <= KB)
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) rs16_matrix_kernel(Rs16MatArgs a) {
+__global__ void __launch_bounds__(kMatBT) __attribute__((amdgpu_waves_per_eu(TEC_RS16_MAT_WPE)))
+rs16_matrix_kernel(Rs16MatArgs a) {
+    constexpr int E = kMatE;
     extern __shared__ __attribute__((aligned(16))) uint16_t lds16[];
     {
         const uint32_t n16 = a.k * (uint32_t)G * 32u;  // 16-byte units of the image
@@ -390,7 +400,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     }
     __syncthreads();
     const uint8_t *tab = reinterpret_cast<const uint8_t *>(lds16);
-    const uint32_t pairs = a.elems >> 1, tps = (pairs + blockDim.x - 1) / blockDim.x;
+    const uint32_t units = a.elems / E, tps = (units + blockDim.x - 1) / blockDim.x;
     const uint32_t ntiles = a.segments * tps;
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {  // no barrier in the loop
         // k and the strides re-read opaquely per tile: loop-invariant, the per-input and per-row
@@ -399,43 +409,57 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
         uint32_t k = a.k, rstride = a.rstride;
         uint64_t in_stride = a.in_stride, out_stride = a.out_stride;
         asm volatile("" : "+s"(k), "+s"(rstride), "+s"(in_stride), "+s"(out_stride));
-        const uint32_t seg = tile / tps, p = (tile - seg * tps) * blockDim.x + threadIdx.x;
-        if (p >= pairs) continue;
-        const uint32_t e0 = 2u * p, eo = (e0 >> 5) * 64u + (e0 & 31u);
+        const uint32_t seg = tile / tps, u = (tile - seg * tps) * blockDim.x + threadIdx.x;
+        if (u >= units) continue;
+        const uint32_t e0 = E * u, eo = (e0 >> 5) * 64u + (e0 & 31u);
         auto inp = [&](uint32_t r) -> const uint8_t * {
             if constexpr (PTRS) return a.ptr[seg * (k + a.rows) + r] + eo;
             else return a.in + (uint64_t)seg * a.seg_in + (uint64_t)r * in_stride + eo;
         };
-        uint32_t acc0[2 * G], acc1[2 * G];
+        uint32_t acc[E][2 * G];
 #pragma unroll
-        for (int i = 0; i < 2 * G; i++) acc0[i] = acc1[i] = 0;
-        // every input's two 16-bit words loaded up front (KB >= k slots, indices past k - 1 clamped),
-        // both elements packed into one VGPR (x0 | x1 << 16, one v_perm), and all of them pinned
-        // here by an empty asm: otherwise the compiler sinks each load into the run-time-guarded
-        // block that uses it and waits for it there, one HBM latency per input (a rolling prefetch
-        // in a loop fared no better: its waits came out as vmcnt(0)).  One wait per tile; the
-        // other waves on the CU cover it.
-        uint32_t P[KB];
+        for (int e = 0; e < E; e++)
+#pragma unroll
+            for (int i = 0; i < 2 * G; i++) acc[e][i] = 0;
+        // every input loaded up front (KB >= k slots, indices past k - 1 clamped), 32 bits of
+        // elements per VGPR (E = 2: both elements of one input, one v_perm; E = 1: two inputs), and
+        // all of them pinned here by an empty asm: otherwise the compiler sinks each load into the
+        // run-time-guarded block that uses it and waits for it there, one HBM latency per input (a
+        // rolling prefetch in a loop fared no better: its waits came out as vmcnt(0)).  One wait
+        // per tile; the other waves on the CU cover it.
+        constexpr int NW = E == 2 ? KB : KB / 2;
+        uint32_t P[NW];
 #pragma unroll
         for (int j = 0; j < KB; j++) {
             const uint8_t *s = inp((uint32_t)j < k ? (uint32_t)j : k - 1u);
-            const uint32_t lo = *reinterpret_cast<const uint16_t *>(s), hi = *reinterpret_cast<const uint16_t *>(s + 32);
-            P[j] = __builtin_amdgcn_perm(hi, lo, 0x05010400u);  // [lo.b0, hi.b0, lo.b1, hi.b1]
+            if constexpr (E == 2) {
+                const uint32_t lo = *reinterpret_cast<const uint16_t *>(s), hi = *reinterpret_cast<const uint16_t *>(s + 32);
+                P[j] = __builtin_amdgcn_perm(hi, lo, 0x05010400u);  // [lo.b0, hi.b0, lo.b1, hi.b1]
+            } else {
+                const uint32_t x = (uint32_t)s[0] | (uint32_t)s[32] << 8;
+                P[j >> 1] = (j & 1) ? P[j >> 1] | x << 16 : x;
+            }
         }
 #pragma unroll
-        for (int j = 0; j < KB; j++) asm volatile("" ::"v"(P[j]));
+        for (int j = 0; j < NW; j++) asm volatile("" ::"v"(P[j]));
 #pragma unroll
         for (int r = 0; r < KB; r++)
-            if ((uint32_t)r < k) mat_input<G>(acc0, acc1, tab + r * rstride, P[r]);
+            if ((uint32_t)r < k) mat_input<G, E>(acc, tab + r * rstride, E == 2 ? P[r] : P[r >> 1], E == 2 ? 0 : 16 * (r & 1));
 #pragma unroll
         for (int i = 0; i < 4 * G; i++) {
             if ((uint32_t)i >= a.rows) continue;
-            const uint32_t v0 = (acc0[i >> 1] >> (16 * (i & 1))) & 0xffffu, v1 = (acc1[i >> 1] >> (16 * (i & 1))) & 0xffffu;
             uint8_t *o;
             if constexpr (PTRS) o = const_cast<uint8_t *>(a.ptr[seg * (k + a.rows) + k + i]) + eo;
             else o = a.out + (uint64_t)seg * a.seg_out + (uint64_t)i * out_stride + eo;
-            *reinterpret_cast<uint16_t *>(o) = (uint16_t)((v0 & 0xffu) | (v1 & 0xffu) << 8);
-            *reinterpret_cast<uint16_t *>(o + 32) = (uint16_t)((v0 >> 8) | (v1 & 0xff00u));
+            const uint32_t v0 = (acc[0][i >> 1] >> (16 * (i & 1))) & 0xffffu;
+            if constexpr (E == 2) {
+                const uint32_t v1 = (acc[E - 1][i >> 1] >> (16 * (i & 1))) & 0xffffu;
+                *reinterpret_cast<uint16_t *>(o) = (uint16_t)((v0 & 0xffu) | (v1 & 0xffu) << 8);
+                *reinterpret_cast<uint16_t *>(o + 32) = (uint16_t)((v0 >> 8) | (v1 & 0xff00u));
+            } else {
+                o[0] = (uint8_t)v0;
+                o[32] = (uint8_t)(v0 >> 8);
+            }
         }
     }
 }
@@ -446,8 +470,8 @@ hipError_t launch_mat_gk(Rs16MatArgs a, uint32_t grid, size_t lds, hipStream_t s
     const void *fn = a.ptrs ? reinterpret_cast<const void *>(rs16_matrix_kernel<G, KB, true>)
                             : reinterpret_cast<const void *>(rs16_matrix_kernel<G, KB, false>);
     if (const hipError_t e = ensure_dyn_lds(fn, lds); e != hipSuccess) return e;
-    if (a.ptrs) hipLaunchKernelGGL((rs16_matrix_kernel<G, KB, true>), dim3(grid), dim3(512), lds, s, a);
-    else hipLaunchKernelGGL((rs16_matrix_kernel<G, KB, false>), dim3(grid), dim3(512), lds, s, a);
+    if (a.ptrs) hipLaunchKernelGGL((rs16_matrix_kernel<G, KB, true>), dim3(grid), dim3(kMatBT), lds, s, a);
+    else hipLaunchKernelGGL((rs16_matrix_kernel<G, KB, false>), dim3(grid), dim3(kMatBT), lds, s, a);
     return hipGetLastError();
 }
 template <int G>
@@ -621,7 +645,7 @@ hipError_t launch_rs16_matrix(const Rs16MatArgs &a, hipStream_t s) {
     if (a.elems == 0 || a.segments == 0) return hipSuccess;
     if (!rs16_mat_supported(a.k, a.rows) || a.elems % 2) return hipErrorInvalidValue;
     if (a.ptrs && (uint64_t)a.segments * (a.k + a.rows) > kRs16DecPtrs) return hipErrorInvalidValue;
-    const uint64_t tiles = (uint64_t)a.segments * (((a.elems >> 1) + 511) / 512);
+    const uint64_t tiles = (uint64_t)a.segments * ((a.elems / rs16k::kMatE + rs16k::kMatBT - 1) / rs16k::kMatBT);
     if (tiles > 0xffffffffull) return hipErrorInvalidValue;
     // a resident grid (2 blocks per CU at the largest image) looping over the tiles: the image is
     // staged once per block, not once per 1,024 columns
