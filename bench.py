@@ -93,7 +93,11 @@ KERNELS = {
     "decode": ["tec_dec_fixed"],  # the pattern kernels (dec_rtc.cpp); random patterns / --decode-jit off: table-driven
     "commit": ["tec::commit::leaf_kernel", "tec::commit::tree_kernel"],
     "recover": ["tec::dstage::dec_stage_kernel<7, 2, 1>"],  # the fused decode writing only the lost slices
+    "outer": ["tec::rs16k::rs16_matrix_kernel<9, 32, false>"],  # OuterCoder(17, 50) encode: 17 x 33 matrix
+    "outer_decode": ["tec::rs16k::rs16_matrix_kernel<5, 32, true>"],  # 17 restored from 17 (3 launches per step)
 }
+# launches of a KERNELS entry per bench step (traffic.py scales its per-launch average by this)
+LAUNCHES_PER_STEP = {"outer_decode": 3}
 
 
 def kernel_names(mode: str, decode_jit: str = "async", pattern: str = "worst") -> list:
@@ -811,6 +815,18 @@ def outer_bench(args, torch, dist, world, rank, dev):
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         cpu = cpu_baseline_outer(args, d_in, d_out, k, m, cb, segs)
+    # PMC bytes per step (scripts/profile_modes.sh outer -> traffic.py), when measured at this shape
+    traffic = {"outer": None, "outer_decode": None}
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            for key in traffic:
+                e = tj.get(key, {})
+                if e.get("objects") == segs and e.get("kernels") == KERNELS[key]:
+                    traffic[key] = e.get("hbm_bytes_per_step")
+        except Exception:
+            pass
+    decode["roofline"]["traffic"] = traffic["outer_decode"]
     if rank == 0:
         print(json.dumps({
             "metric": "device-resident OuterCoder(17, 50) encode GiB/s of snapshot data, 4 MiB chunks, 1 MI355X",
@@ -822,7 +838,7 @@ def outer_bench(args, torch, dist, world, rank, dev):
                                    "(reed-solomon-simd Leopard GF(2^16) construction, parity unpinned)",
                        "segments_per_gpu": segs, "chunk_bytes": cb, "parallelism": f"segments over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": round(alg / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(alg / avg_s / 1e9 / PEAK_HBM_GBS, 4), "traffic": None,
+                         "frac": round(alg / avg_s / 1e9 / PEAK_HBM_GBS, 4), "traffic": traffic["outer"],
                          "alg_bytes_per_launch": alg, "avg_launch_ms": round(avg_s * 1e3, 4)},
             "cpu_baseline": cpu, "outputs_verified": verified, "decode": decode}), flush=True)
     if world > 1:

@@ -39,7 +39,7 @@ def per_step(d, m):
             disp = per.setdefault(key, {})
             disp[r.get("Dispatch_Id", "")] = disp.get(r.get("Dispatch_Id", ""), 0.0) + float(r["Counter_Value"])
         for (kn, c), disp in per.items():
-            tot[c] = tot.get(c, 0.0) + sum(disp.values()) / len(disp)
+            tot[c] = tot.get(c, 0.0) + sum(disp.values()) / len(disp) * bench.LAUNCHES_PER_STEP.get(m, 1)
     return tot
 
 
@@ -51,7 +51,7 @@ def main():
     if "mode" in out:  # the round-1 single-mode layout
         out = {}
     for m in modes:
-        c = per_step(os.path.join(root, m.replace(":", "_")), m)
+        c = per_step(os.path.join(root, (m if m != "outer_decode" else "outer").replace(":", "_")), m)
         if not c:
             print(m, "no counters")
             continue
