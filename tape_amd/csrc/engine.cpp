@@ -3574,11 +3574,19 @@ int te_slicer_repair(te_clay *c, const te_repair_plan *p, const uint8_t *const *
     for (uint32_t sl = 0; sl < p->n; sl++)
         if (need[sl]) segs.push_back({c->hio_in.u8() + off[sl], helper_data[sl], need[sl]});
     CopyPool::get().run(segs);
-    TE_HIP(hipMemcpyAsync(c->io_in.p, c->hio_in.p, total, hipMemcpyHostToDevice, c->stream));
+    // measurement option (TEC_DEBUG_KNOBS=1 TEC_REPAIR_ZC=1): the kernels read the helpers from and
+    // write the slice to the pinned staging directly, over PCIe, with no H2D / D2H copy
+    static const bool zc = [] { const char *e = tec_knob("TEC_REPAIR_ZC"); return e && e[0] == '1'; }();
     RepItem it{p, off.data(), 0, metadata};
-    r = repair_enqueue(c, c->io_in.as<uint8_t>(), &it, 1, c->io_out.as<uint8_t>(), c->stream);
-    if (r) return r;
-    TE_HIP(hipMemcpyAsync(c->hio_out.p, c->io_out.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
+    if (zc) {
+        r = repair_enqueue(c, c->hio_in.u8(), &it, 1, c->hio_out.u8(), c->stream);
+        if (r) return r;
+    } else {
+        TE_HIP(hipMemcpyAsync(c->io_in.p, c->hio_in.p, total, hipMemcpyHostToDevice, c->stream));
+        r = repair_enqueue(c, c->io_in.as<uint8_t>(), &it, 1, c->io_out.as<uint8_t>(), c->stream);
+        if (r) return r;
+        TE_HIP(hipMemcpyAsync(c->hio_out.p, c->io_out.p, out_bytes, hipMemcpyDeviceToHost, c->stream));
+    }
     TE_HIP(hipStreamSynchronize(c->stream));  // (an event spin-wait measured no better: 0.146 vs 0.132-0.139 ms, r05)
     // (pipelining the gather with the H2D in four pieces and the scatter with the D2H in two
     // halves measured slower: 0.17 against 0.134-0.143 ms per 4 MiB call, r05)
