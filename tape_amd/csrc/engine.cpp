@@ -3574,9 +3574,11 @@ int te_slicer_repair(te_clay *c, const te_repair_plan *p, const uint8_t *const *
     for (uint32_t sl = 0; sl < p->n; sl++)
         if (need[sl]) segs.push_back({c->hio_in.u8() + off[sl], helper_data[sl], need[sl]});
     CopyPool::get().run(segs);
-    // measurement option (TEC_DEBUG_KNOBS=1 TEC_REPAIR_ZC=1): the kernels read the helpers from and
-    // write the slice to the pinned staging directly, over PCIe, with no H2D / D2H copy
-    static const bool zc = [] { const char *e = tec_knob("TEC_REPAIR_ZC"); return e && e[0] == '1'; }();
+    // the kernels read the helpers from and write the slice to the pinned staging directly, over
+    // PCIe, with no H2D / D2H copy: 0.131 -> 0.103 ms per 4 MiB call, 0.85 -> 0.73 ms at 64 MiB
+    // (r05, scripts/gpu_percall_zc.sh; the repair kernels only read their inputs and write their
+    // output once).  Measurement option TEC_DEBUG_KNOBS=1 TEC_REPAIR_ZC=0: the copies instead.
+    static const bool zc = [] { const char *e = tec_knob("TEC_REPAIR_ZC"); return !(e && e[0] == '0'); }();
     RepItem it{p, off.data(), 0, metadata};
     if (zc) {
         r = repair_enqueue(c, c->hio_in.u8(), &it, 1, c->hio_out.u8(), c->stream);
