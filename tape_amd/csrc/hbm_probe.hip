@@ -10,7 +10,9 @@
 //                       range in whole 1 KiB wave-blocks (16 B per lane, nt stores);
 //   shape 1 ("rows"):   the same, but the output walks 1,430-byte rows from a 2-aligned start, two
 //                       store instructions per row -- the slices' sub-chunk rows, as the encode
-//                       kernel writes them.
+//                       kernel writes them;
+//   shape 2 ("rows, aligned interior"): the same rows, their 16-byte-aligned interior as aligned
+//                       16-byte pieces and the partial head / tail as 2-byte stores (measurement).
 // A kernel can at best reach the "blocks" figure; "rows" is what the slices' row shape alone costs.
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -19,7 +21,8 @@ namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <bool ROWS>
+template <int ROWS>  // 0 blocks, 1 rows (16-B pieces from the 2-aligned row start), 2 rows with
+                    // 16-B-aligned interior pieces and 2-byte stores for the partial head / tail
 __global__ void __launch_bounds__(256) mix_kernel(const uint8_t *in, uint64_t in_per_wg, uint8_t *out,
                                                   uint64_t out_per_wg, uint32_t *sink) {
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -39,7 +42,15 @@ __global__ void __launch_bounds__(256) mix_kernel(const uint8_t *in, uint64_t in
         // this iteration's share of the output, in proportion (reads : writes as in the encode)
         const uint32_t w0 = (uint32_t)((uint64_t)it * nout / iters), w1 = (uint32_t)((uint64_t)(it + 1) * nout / iters);
         for (uint32_t b = w0 + wv; b < w1; b += 4) {
-            if constexpr (ROWS) {
+            if constexpr (ROWS == 2) {
+                const uint32_t a0 = 2 + b * 1430u, e0 = a0 + 1430u, A = (a0 + 15u) & ~15u, E = e0 & ~15u;
+                const uint32_t n16 = (E - A) >> 4;
+                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)(lane < n16 ? A + lane * 16u : 0x80000000u), 0, 2);
+                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)(lane + 64u < n16 ? A + (lane + 64u) * 16u : 0x80000000u), 0, 2);
+                const uint32_t nh = (A - a0) >> 1, nt = (e0 - E) >> 1;
+                const uint32_t o2 = lane < nh ? a0 + 2u * lane : (lane >= 8 && lane - 8u < nt ? E + 2u * (lane - 8u) : 0x80000000u);
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)lane, wb, (int)o2, 0, 2);
+            } else if constexpr (ROWS == 1) {
                 const uint32_t base = 2 + b * 1430u;
                 __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)(lane * 16), (int)base, 2);
                 const uint32_t o1 = lane < 25 ? 1024u + 16u * lane : (lane == 25 ? 1430u - 16u : 0x80000000u);
@@ -69,14 +80,17 @@ extern "C" int tec_probe_encode_mix(const void *in, uint64_t in_bytes, void *out
         if (e != hipSuccess) return (int)e;
     }
     const uint64_t ipw = (in_bytes / (uint64_t)wgs) & ~(uint64_t)1023;
-    const uint64_t opw = shape ? out_bytes / (uint64_t)wgs : (out_bytes / (uint64_t)wgs) & ~(uint64_t)1023;
+    const uint64_t opw = shape ? (out_bytes / (uint64_t)wgs) & ~(uint64_t)15 : (out_bytes / (uint64_t)wgs) & ~(uint64_t)1023;
     if (ipw >= (1ull << 31) || opw >= (1ull << 31)) return (int)hipErrorInvalidValue;
     auto launch = [&] {
-        if (shape)
-            hipLaunchKernelGGL(mix_kernel<true>, dim3(wgs), dim3(256), 0, s, (const uint8_t *)in, ipw, (uint8_t *)out,
+        if (shape == 2)
+            hipLaunchKernelGGL(mix_kernel<2>, dim3(wgs), dim3(256), 0, s, (const uint8_t *)in, ipw, (uint8_t *)out,
+                               opw, g_sink);
+        else if (shape)
+            hipLaunchKernelGGL(mix_kernel<1>, dim3(wgs), dim3(256), 0, s, (const uint8_t *)in, ipw, (uint8_t *)out,
                                opw, g_sink);
         else
-            hipLaunchKernelGGL(mix_kernel<false>, dim3(wgs), dim3(256), 0, s, (const uint8_t *)in, ipw, (uint8_t *)out,
+            hipLaunchKernelGGL(mix_kernel<0>, dim3(wgs), dim3(256), 0, s, (const uint8_t *)in, ipw, (uint8_t *)out,
                                opw, g_sink);
     };
     hipEvent_t e0, e1;
