@@ -45,9 +45,15 @@ constexpr int kWaves = G + 1;              // six compute waves and a loader wav
 // compute waves keep at most this many stores in flight before B1, so every slice row a
 // later DMA reads back (level-2 partners, >= 8 steps later) has landed: <= 3 steps of stores
 constexpr int kCap = 5;  // flush rows per wave per step
-constexpr int kStoreLag = 30;
+#ifndef TEC_DMA_STORELAG
+#define TEC_DMA_STORELAG 30
+#endif
+constexpr int kStoreLag = TEC_DMA_STORELAG;
 static_assert(kStoreLag <= 3 * 2 * kCap && kStoreLag < 64, "stores older than 3 steps must have landed");
 constexpr uint32_t kDrop = 0x80000000u;    // offset past every resource: the range check drops it
+#ifndef TEC_DMA_JX
+#define TEC_DMA_JX 0  // 1: measurement only, junction-line pricing (writes wrong bytes)
+#endif
 #ifndef TEC_DMA_ST_AUX
 #define TEC_DMA_ST_AUX 2
 #endif
@@ -235,6 +241,12 @@ __global__ void __launch_bounds__(kWaves * 64, 4) enc_dma_kernel(EncArgs a) {
     const uint32_t dst_range = a.n * slen - J.dst_skew;  // < 2^31, host-checked
     const u32x4 rs_dst = rsrc(J.dst, dst_range);
     const __amdgpu_buffer_rsrc_t rb_dst = __builtin_amdgcn_make_buffer_rsrc(J.dst, 0, (int)dst_range, 0x00020000);
+#if TEC_DMA_JX
+    // (measurement) the destination base's line offset, and a resource from the line it starts in
+    const uint32_t jx_base = (uint32_t)(reinterpret_cast<uintptr_t>(J.dst) & 127u);
+    const __amdgpu_buffer_rsrc_t rb_jx =
+        __builtin_amdgcn_make_buffer_rsrc(J.dst - jx_base, 0, (int)(dst_range + jx_base), 0x00020000);
+#endif
     const uint32_t store_mask = J.store_mask;  // chunks to write (internal nodes)
     uint32_t sl_lane = lane + J.rot;
     sl_lane = (sl_lane >= 20u ? sl_lane - 20u : sl_lane) * slen;
@@ -461,8 +473,18 @@ __global__ void __launch_bounds__(kWaves * 64, 4) enc_dma_kernel(EncArgs a) {
 #pragma unroll
             for (int q = 0; q < kCap; q++) {
                 if ((uint32_t)q < n) {
+#if TEC_DMA_JX
+                    // measurement only (wrong bytes): the row's stores as whole 128-B lines, every
+                    // junction line once -- the write pattern of line-exact stores, to price them
+                    const uint32_t ab = jx_base + dst[q], first = (ab + 127u) & ~127u;
+                    const uint32_t o0 = first + 16u * lane - jx_base, o1 = first + 16u * (64u + lane) - jx_base;
+                    const uint32_t lim = ((ab + (uint32_t)sc + 127u) & ~127u) - jx_base;
+                    __builtin_amdgcn_raw_buffer_store_b128(d0[q], rb_jx, (int)(dst[q] == kDrop ? kDrop : o0), 0, kStAux);
+                    __builtin_amdgcn_raw_buffer_store_b128(d1[q], rb_jx, (int)(dst[q] == kDrop || o1 >= lim ? kDrop : o1), 0, kStAux);
+#else
                     __builtin_amdgcn_raw_buffer_store_b128(d0[q], rb_dst, (int)vo0, (int)dst[q], kStAux);
                     __builtin_amdgcn_raw_buffer_store_b128(d1[q], rb_dst, (int)vo1, (int)dst[q], kStAux);
+#endif
                 }
             }
         }

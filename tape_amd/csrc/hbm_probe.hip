@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(256) mix_kernel(const uint8_t *in, uint64_t in
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(src), 0, (int)in_per_wg, 0x00020000);
     const __amdgpu_buffer_rsrc_t wb = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)out_per_wg, 0x00020000);
     const uint32_t nin = (uint32_t)(in_per_wg / 1024);
-    const uint32_t nout = (uint32_t)(ROWS ? (out_per_wg - 2) / 1430 : out_per_wg / 1024);
+    const uint32_t nout = (uint32_t)(ROWS == 5 ? out_per_wg / 1408 : ROWS ? (out_per_wg - 2) / 1430 : out_per_wg / 1024);
     const uint32_t iters = (nin + 3) / 4;
     u32x4 acc = {0, 0, 0, 0};
     const u32x4 v = {lane, wv, 7u, 9u};
@@ -50,11 +50,28 @@ __global__ void __launch_bounds__(256) mix_kernel(const uint8_t *in, uint64_t in
                 const uint32_t nh = (A - a0) >> 1, nt = (e0 - E) >> 1;
                 const uint32_t o2 = lane < nh ? a0 + 2u * lane : (lane >= 8 && lane - 8u < nt ? E + 2u * (lane - 8u) : 0x80000000u);
                 __builtin_amdgcn_raw_buffer_store_b16((uint16_t)lane, wb, (int)o2, 0, 2);
-            } else if constexpr (ROWS == 1) {
+            } else if constexpr (ROWS == 1 || ROWS == 3) {  // 3: the same with the default (write-back) policy
+                constexpr int aux = ROWS == 1 ? 2 : 0;
                 const uint32_t base = 2 + b * 1430u;
-                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)(lane * 16), (int)base, 2);
+                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)(lane * 16), (int)base, aux);
                 const uint32_t o1 = lane < 25 ? 1024u + 16u * lane : (lane == 25 ? 1430u - 16u : 0x80000000u);
-                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)o1, (int)base, 2);
+                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)o1, (int)base, aux);
+            } else if constexpr (ROWS == 5) {  // whole-line rows: 1,408 B (11 lines) from 128-B-aligned starts, 64 + 24 lanes
+                const uint32_t base = b * 1408u;
+                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)(lane * 16), (int)base, 2);
+                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)(lane < 24 ? 1024u + 16u * lane : 0x80000000u), (int)base, 2);
+            } else if constexpr (ROWS == 4) {  // nt interior, write-back for the two pieces in the junction lines
+                const uint32_t base = 2 + b * 1430u;
+                const uint32_t o1 = lane < 25 ? 1024u + 16u * lane : (lane == 25 ? 1430u - 16u : 0x80000000u);
+                // pieces inside the row's partial first / last 128-B line (shared with the neighbour row)
+                const uint32_t ab = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 127u) + base, ae = ab + 1430u;
+                const uint32_t first_end = (ab & 127u) ? (ab + 127u) & ~127u : ab, last_beg = (ae & 127u) ? ae & ~127u : ae;
+                const uint32_t p0 = ab + lane * 16u, p1 = ab + o1;
+                const bool j0 = p0 < first_end || p0 + 16u > last_beg, j1 = o1 != 0x80000000u && (p1 < first_end || p1 + 16u > last_beg);
+                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)(j0 ? 0x80000000u : lane * 16), (int)base, 2);
+                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)(j0 ? 0u : 0x80000000u), (int)base, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)(j1 ? 0x80000000u : o1), (int)base, 2);
+                __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)(j1 ? o1 : 0x80000000u), (int)base, 0);
             } else {
                 __builtin_amdgcn_raw_buffer_store_b128(v, wb, (int)(b * 1024 + lane * 16), 0, 2);
             }
@@ -80,10 +97,20 @@ extern "C" int tec_probe_encode_mix(const void *in, uint64_t in_bytes, void *out
         if (e != hipSuccess) return (int)e;
     }
     const uint64_t ipw = (in_bytes / (uint64_t)wgs) & ~(uint64_t)1023;
-    const uint64_t opw = shape ? (out_bytes / (uint64_t)wgs) & ~(uint64_t)15 : (out_bytes / (uint64_t)wgs) & ~(uint64_t)1023;
+    const uint64_t opw = shape == 5 ? (out_bytes / (uint64_t)wgs) & ~(uint64_t)127
+                         : shape ? (out_bytes / (uint64_t)wgs) & ~(uint64_t)15 : (out_bytes / (uint64_t)wgs) & ~(uint64_t)1023;
     if (ipw >= (1ull << 31) || opw >= (1ull << 31)) return (int)hipErrorInvalidValue;
     auto launch = [&] {
-        if (shape == 2)
+        if (shape == 5)
+            hipLaunchKernelGGL(mix_kernel<5>, dim3(wgs), dim3(256), 0, s, (const uint8_t *)in, ipw, (uint8_t *)out,
+                               opw, g_sink);
+        else if (shape == 4)
+            hipLaunchKernelGGL(mix_kernel<4>, dim3(wgs), dim3(256), 0, s, (const uint8_t *)in, ipw, (uint8_t *)out,
+                               opw, g_sink);
+        else if (shape == 3)
+            hipLaunchKernelGGL(mix_kernel<3>, dim3(wgs), dim3(256), 0, s, (const uint8_t *)in, ipw, (uint8_t *)out,
+                               opw, g_sink);
+        else if (shape == 2)
             hipLaunchKernelGGL(mix_kernel<2>, dim3(wgs), dim3(256), 0, s, (const uint8_t *)in, ipw, (uint8_t *)out,
                                opw, g_sink);
         else if (shape)
