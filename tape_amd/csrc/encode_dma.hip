@@ -223,7 +223,12 @@ __global__ void __launch_bounds__(kWaves * 64, 4) enc_dma_kernel(EncArgs a) {
     const uint32_t lane = threadIdx.x & 63;
 
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
-    const EncJob J = a.jobs[tile];
+    const uint32_t split = a.z0_split ? a.z0_split : 1u;
+    const uint32_t job = tile / split, part = tile - job * split;
+    const uint32_t z0b = a.z0_count ? a.z0_first + part * a.z0_count : 0u;
+    const uint32_t z0e = a.z0_count ? z0b + a.z0_count : (uint32_t)kQ;
+    const uint32_t zb = z0b * kQ, ze = z0e * kQ;  // this workgroup's planes [zb, ze)
+    const EncJob J = a.jobs[job];
     const uint32_t cs = a.cs, sc = a.sc, slen = a.slice_len;
     // lane word: columns 4w..4w+3 of every row; words past the 1,440-column image alias the
     // last one (same inputs, same values, same staging address)
@@ -363,24 +368,27 @@ __global__ void __launch_bounds__(kWaves * 64, 4) enc_dma_kernel(EncArgs a) {
     if (wv == (uint32_t)G) {
         // the loader: every plane's DMA, two planes ahead of the compute; the barriers mirror
         // the compute waves' B2 / B1 (the ring slot of plane z is free after B1 of z)
-        issue_dma(0, 0);
-        issue_dma(1, kSlotBytes);
-        if constexpr (TEC_DMA_ROWPOL != 0)
+        issue_dma(zb, 0);  // zb is even: plane z uses ring slot z & 1
+        issue_dma(zb + 1u, kSlotBytes);
+        if (zb != 0)  // a level-2 start (split launch) issues fewer rows per plane: wait for both
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        else if constexpr (TEC_DMA_ROWPOL != 0)
             asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");  // plane 0 landed (16 rows x 2)
         else
             asm volatile("s_waitcnt vmcnt(23)\n\ts_barrier" ::: "memory");  // plane 0 landed
-        for (uint32_t z = 0; z < (uint32_t)(kQ * kQ); z++) {
+        // the same number of iterations as the compute waves' plane loop: two barriers each
+        for (uint32_t z = zb; z < ze; z++) {
             lds_barrier();                                  // B2
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // plane z + 1 landed
             lds_barrier();                                  // B1
-            if (z + 2u < (uint32_t)(kQ * kQ)) issue_dma(z + 2u, (z & 1u) * kSlotBytes);
+            if (z + 2u < ze) issue_dma(z + 2u, (z & 1u) * kSlotBytes);
         }
         return;
     }
     asm volatile("s_barrier" ::: "memory");
 
     uint8_t *const stg = lds8 + kStageBase + colw;
-    for (uint32_t z0 = 0; z0 < (uint32_t)kQ; z0++) {
+    for (uint32_t z0 = z0b; z0 < z0e; z0++) {
         const bool lvl2 = z0 >= (uint32_t)K;
         const uint32_t type = lvl2 ? z0 - (K - 1) : 0u;
         for (uint32_t s = 0; s < (uint32_t)kQ; s++) {
@@ -490,7 +498,7 @@ __global__ void __launch_bounds__(kWaves * 64, 4) enc_dma_kernel(EncArgs a) {
         }
     }
     // the last plane's left-over row (its staging row is untouched since the last compute)
-    if (wv == 0) {
+    if (wv == 0 && z0e == (uint32_t)kQ) {
         const uint32_t it = kFlush.extra, src = it & 0xffu;
         const uint8_t *row = lds8 + kStageBase + src * RW;
         const u32x4 e0 = *reinterpret_cast<const u32x4 *>(row + lo0);
@@ -513,12 +521,20 @@ hipError_t launch_encode_dma(bool masked, const EncArgs &a, hipStream_t s) {
     if (!encode_dma_supported((int)a.n, 7, a.sc) || a.njobs > 0x7fffffffu) return hipErrorInvalidValue;
     const void *fn = masked ? reinterpret_cast<const void *>(dma::enc_dma_kernel<true>)
                             : reinterpret_cast<const void *>(dma::enc_dma_kernel<false>);
-    hipError_t e = ensure_dyn_lds(fn, dma::kLdsBytes);
+#ifndef TEC_DMA_LDS_PAD
+#define TEC_DMA_LDS_PAD 0  // measurement: extra dynamic LDS (e.g. 40960 -> one workgroup per CU)
+#endif
+    const size_t lds = dma::kLdsBytes + TEC_DMA_LDS_PAD;
+    hipError_t e = ensure_dyn_lds(fn, lds);
     if (e != hipSuccess) return e;
+    // a plane range must start on an even plane (ring slot parity) and stay within the 100 planes
+    if (a.z0_count && (a.z0_split == 0 || a.z0_first + a.z0_split * a.z0_count > 10u)) return hipErrorInvalidValue;
+    const uint64_t grid = (uint64_t)a.njobs * (a.z0_count ? a.z0_split : 1u);
+    if (grid > 0x7fffffffu) return hipErrorInvalidValue;
     if (masked)
-        hipLaunchKernelGGL(dma::enc_dma_kernel<true>, dim3(a.njobs), dim3(dma::kWaves * 64), dma::kLdsBytes, s, a);
+        hipLaunchKernelGGL(dma::enc_dma_kernel<true>, dim3((uint32_t)grid), dim3(dma::kWaves * 64), lds, s, a);
     else
-        hipLaunchKernelGGL(dma::enc_dma_kernel<false>, dim3(a.njobs), dim3(dma::kWaves * 64), dma::kLdsBytes, s, a);
+        hipLaunchKernelGGL(dma::enc_dma_kernel<false>, dim3((uint32_t)grid), dim3(dma::kWaves * 64), lds, s, a);
     return hipGetLastError();
 }
 

@@ -47,6 +47,14 @@ const bool g_no_dma_encode = [] {
 // Measured slower (r05 trace of --mode percall: 438 us per 4 MiB object against 296 us for the
 // LDS-DMA kernel -- a lone stripe is bound by the 100-plane chain's latency, not its work per
 // step), so it is off (0); measurement only.
+// Per-call encodes of at most this many 1 MB stripes run the LDS-DMA kernel split in two launches:
+// the seven level-1 plane rows of a stripe on seven workgroups, then the level-2 chain on one --
+// a lone stripe is latency-bound by its 100-plane chain (296 us per 4 MiB object).  Measurement
+// option TEC_DEBUG_KNOBS=1 TEC_ENC_SPLIT=n (0: never).
+const uint32_t g_enc_split = [] {
+    const char *e = tec_knob("TEC_ENC_SPLIT");
+    return e ? (uint32_t)atoi(e) : 64u;
+}();
 const uint32_t g_enc_small = [] {
     const char *e = tec_knob("TEC_ENC_SMALL");
     return e ? (uint32_t)atoi(e) : 0u;
@@ -1068,6 +1076,11 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
             a.sc = sc;
             a.slice_len = (uint32_t)L.key.slice_len;
             a.n = (uint32_t)n;
+            if (per_call && total_stripes <= g_enc_split) {
+                a.z0_first = 0; a.z0_count = 1; a.z0_split = 7;   // level-1 rows z0 = 0..6, one workgroup each
+                TE_HIP(launch_encode_dma(L.key.masked, a, s));
+                a.z0_first = 7; a.z0_count = 3; a.z0_split = 1;   // level 2 reads their parity back
+            }
             TE_HIP(launch_encode_dma(L.key.masked, a, s));
         } else if (fast_path(L)) {
             (void)full;

@@ -45,6 +45,11 @@ struct EncArgs {
     uint32_t slice_len;
     uint32_t n;
     uint8_t *scratch;      // level-2 parking, encode_rows_scratch_bytes() bytes
+    // encode_dma.hip: rows of planes z0 = z0_first + part * z0_count .. + z0_count, part < z0_split
+    // (z0_split workgroups per stripe); z0_count 0 = all ten.  The level-1 rows (z0 < 7) are
+    // independent of each other, so a small call runs them on 7 workgroups per stripe and the
+    // level-2 rows (7..9, a chain) in a second launch.
+    uint32_t z0_first, z0_count, z0_split;
 };
 
 // Metadata suffix writer: one 48-byte record per object, copied to its n slices.
