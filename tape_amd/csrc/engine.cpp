@@ -53,7 +53,7 @@ const bool g_no_dma_encode = [] {
 // option TEC_DEBUG_KNOBS=1 TEC_ENC_SPLIT=n (0: never).
 const uint32_t g_enc_split = [] {
     const char *e = tec_knob("TEC_ENC_SPLIT");
-    return e ? (uint32_t)atoi(e) : 64u;
+    return e ? (uint32_t)atoi(e) : 512u;
 }();
 const uint32_t g_enc_small = [] {
     const char *e = tec_knob("TEC_ENC_SMALL");
