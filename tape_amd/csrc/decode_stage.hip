@@ -504,19 +504,20 @@ uint32_t decode_stage_rows(uint32_t nslots, uint32_t max_out) { return (TEC_DEC_
 bool decode_stage_fits(uint32_t nslots, uint32_t max_out) { return decode_stage_rows(nslots, max_out) <= dstage::kMaxLdsRows; }
 bool decode_stage_k(int k) { return k >= 7 && k <= 10; }
 
-uint32_t decode_stage_g(uint32_t words_per_stripe) {
+uint32_t decode_stage_g(uint32_t words_per_stripe, uint32_t gmax) {
     const uint32_t groups = (words_per_stripe + 63) / 64;
-    return groups < (uint32_t)dstage::kMaxG ? groups : (uint32_t)dstage::kMaxG;
+    const uint32_t cap = gmax && gmax < (uint32_t)dstage::kMaxG ? gmax : (uint32_t)dstage::kMaxG;
+    return groups < cap ? groups : cap;
 }
 
 // workgroups per stripe: groups of 64 words, g * WPL of them per workgroup
-static uint32_t decode_stage_wgs(uint32_t words_per_stripe) {
-    const uint32_t groups = (words_per_stripe + 63) / 64, g = decode_stage_g(words_per_stripe);
+static uint32_t decode_stage_wgs(uint32_t words_per_stripe, uint32_t gmax) {
+    const uint32_t groups = (words_per_stripe + 63) / 64, g = decode_stage_g(words_per_stripe, gmax);
     return (groups + g * dstage::kWpl - 1) / (g * dstage::kWpl);
 }
 
 size_t decode_stage_scratch_bytes(const DecArgs &a) {
-    const uint32_t g = decode_stage_g(a.words_per_stripe), wgs = decode_stage_wgs(a.words_per_stripe);
+    const uint32_t g = decode_stage_g(a.words_per_stripe, a.gmax), wgs = decode_stage_wgs(a.words_per_stripe, a.gmax);
     return (size_t)a.njobs * wgs * (a.nscratch_max ? a.nscratch_max : 1) * g * 256u * dstage::kWpl;
 }
 
@@ -542,8 +543,8 @@ hipError_t launch_decode_stage(DecArgs a, hipStream_t s) {
     if (a.lds_rows == 0 || a.lds_rows > dstage::kMaxLdsRows || a.sc < 8 || !a.scratch || a.n != 2u * kRepQ ||
         !decode_stage_k((int)a.nk))
         return hipErrorInvalidValue;
-    const uint32_t g = decode_stage_g(a.words_per_stripe);
-    a.wgs_per_stripe = decode_stage_wgs(a.words_per_stripe);
+    const uint32_t g = decode_stage_g(a.words_per_stripe, a.gmax);
+    a.wgs_per_stripe = decode_stage_wgs(a.words_per_stripe, a.gmax);
     const uint64_t blocks = (uint64_t)a.njobs * a.wgs_per_stripe;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     switch (a.nk) {

@@ -55,6 +55,13 @@ const uint32_t g_enc_split = [] {
     const char *e = tec_knob("TEC_ENC_SPLIT");
     return e ? (uint32_t)atoi(e) : 512u;
 }();
+// Measurement option TEC_DEBUG_KNOBS=1 TEC_ENC_SPLIT_BATCH=1: every call split that way (the seven
+// level-1 workgroups of a stripe run side by side on one XCD, so a row one of them reads as its
+// own and another as a partner is read twice at about the same time).
+const bool g_enc_split_batch = [] {
+    const char *e = tec_knob("TEC_ENC_SPLIT_BATCH");
+    return e && e[0] == '1';
+}();
 const uint32_t g_enc_small = [] {
     const char *e = tec_knob("TEC_ENC_SMALL");
     return e ? (uint32_t)atoi(e) : 0u;
@@ -1076,7 +1083,7 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
             a.sc = sc;
             a.slice_len = (uint32_t)L.key.slice_len;
             a.n = (uint32_t)n;
-            if (per_call && total_stripes <= g_enc_split) {
+            if ((per_call && total_stripes <= g_enc_split) || g_enc_split_batch) {
                 a.z0_first = 0; a.z0_count = 1; a.z0_split = 7;   // level-1 rows z0 = 0..6, one workgroup each
                 TE_HIP(launch_encode_dma(L.key.masked, a, s));
                 a.z0_first = 7; a.z0_count = 3; a.z0_split = 1;   // level 2 reads their parity back
@@ -1516,6 +1523,16 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
             S.written_stream = s;
         }
     }
+    // a small call (a per-call decode: a few stripes on a 256-CU chip) runs one wave per
+    // workgroup, so each stripe's 100-step chain is split over more workgroups with less work per
+    // step.  Measurement option TEC_DEBUG_KNOBS=1 TEC_DEC_SMALL=n: the stripe bound (0: never).
+    static const size_t dec_small_max = [] {
+        const char *e = tec_knob("TEC_DEC_SMALL");
+        return e ? (size_t)atoi(e) : (size_t)64;
+    }();
+    size_t call_stripes = 0;
+    for (auto &o : offs) call_stripes += groups[o.first].size();
+    const bool small_dec = call_stripes <= dec_small_max;
     auto dec_args = [&](const std::pair<uint64_t, size_t> &o) {
         const uint64_t cs = o.first >> 32;
         const uint32_t sc = (uint32_t)(cs / (uint64_t)h.alpha);
@@ -1539,6 +1556,7 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         a.nscratch_max = nscr_max;
         a.in_stride = group_in_stride[o.first];
         a.out_stride = cs;
+        a.gmax = small_dec ? 1u : 0u;
         return a;
     };
     auto fixed_args = [&](const Fixed &f, uint8_t *scratch) {

@@ -201,12 +201,13 @@ struct DecArgs {
     uint32_t njobs, words_per_stripe, wgs_per_stripe;
     uint32_t cs, sc, n, nk, lds_rows, nscratch_max;  // lds_rows: max over patterns of slots + staging rows
     uint64_t in_stride, out_stride;
+    uint32_t gmax;  // waves per workgroup at most (0: the build's TEC_DEC_MAXG); 1 for small calls
 };
 hipError_t launch_decode_stage(DecArgs a, hipStream_t s);
 size_t decode_stage_scratch_bytes(const DecArgs &a);
 uint32_t decode_stage_rows(uint32_t nslots, uint32_t max_out);  // LDS rows of a program
 bool decode_stage_fits(uint32_t nslots, uint32_t max_out);
-uint32_t decode_stage_g(uint32_t words_per_stripe);             // waves per workgroup
+uint32_t decode_stage_g(uint32_t words_per_stripe, uint32_t gmax = 0);  // waves per workgroup
 
 // Per-pattern decode kernels compiled at run time (dec_rtc.cpp, dec_fixed.hpp), per handle.
 using dfix_args = dfix::Args;
