@@ -1070,6 +1070,7 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
         return a;
     };
     size_t gi = 0;
+    std::vector<std::pair<bool, EncArgs>> level2;  // split launches' level-2 halves, enqueued last
     for (const Launch &L : launches) {
         const uint32_t cs = (uint32_t)L.key.cs, sc = cs / (uint32_t)h.alpha;
         const uint32_t wps = (sc + 3) / 4;   // words incl. a 2-column tail when sc % 4 == 2
@@ -1086,9 +1087,11 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
             if ((per_call && total_stripes <= g_enc_split) || g_enc_split_batch) {
                 a.z0_first = 0; a.z0_count = 1; a.z0_split = 7;   // level-1 rows z0 = 0..6, one workgroup each
                 TE_HIP(launch_encode_dma(L.key.masked, a, s));
-                a.z0_first = 7; a.z0_count = 3; a.z0_split = 1;   // level 2 reads their parity back
+                a.z0_first = 7; a.z0_count = 3; a.z0_split = 1;   // level 2 reads their parity back:
+                level2.push_back({L.key.masked, a});              // after every level-1 launch
+            } else {
+                TE_HIP(launch_encode_dma(L.key.masked, a, s));
             }
-            TE_HIP(launch_encode_dma(L.key.masked, a, s));
         } else if (fast_path(L)) {
             (void)full;
             EncArgs a{};
@@ -1108,6 +1111,7 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
         }
         gi++;
     }
+    for (const auto &l2 : level2) TE_HIP(launch_encode_dma(l2.first, l2.second, s));
     kt.stop();
     return A.mark_done(s);
 }
@@ -3324,6 +3328,8 @@ int te_slicer_encode(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *data, 
     r = encode_enqueue(c, cfg, c->io_in.as<uint8_t>(), &o, 1, c->io_out.as<uint8_t>(), c->stream, false, nullptr,
                        StripeSel(), true);
     if (r) return r;
+    // (copying the level-1 rows out while level 2 runs, as 2-D copies on a second stream, measured
+    // slower: 0.62 against 0.50 ms pageable, 0.505 against 0.485 pinned, r05)
     TE_HIP(hipMemcpyAsync(slices, c->io_out.p, total, hipMemcpyDeviceToHost, c->stream));
     TE_HIP(hipStreamSynchronize(c->stream));
     return TE_OK;
