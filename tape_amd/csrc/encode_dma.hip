@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(kWaves * 64, 4) enc_dma_kernel(EncArgs a) {
     const uint32_t split = a.z0_split ? a.z0_split : 1u;
     const uint32_t job = tile / split, part = tile - job * split;
     const uint32_t z0b = a.z0_count ? a.z0_first + part * a.z0_count : 0u;
-    const uint32_t z0e = a.z0_count ? z0b + a.z0_count : (uint32_t)kQ;
+    const uint32_t z0e = a.z0_count ? min(z0b + a.z0_count, a.z0_limit ? a.z0_limit : (uint32_t)kQ) : (uint32_t)kQ;
     const uint32_t zb = z0b * kQ, ze = z0e * kQ;  // this workgroup's planes [zb, ze)
     const EncJob J = a.jobs[job];
     const uint32_t cs = a.cs, sc = a.sc, slen = a.slice_len;
@@ -528,7 +528,11 @@ hipError_t launch_encode_dma(bool masked, const EncArgs &a, hipStream_t s) {
     hipError_t e = ensure_dyn_lds(fn, lds);
     if (e != hipSuccess) return e;
     // a plane range must start on an even plane (ring slot parity) and stay within the 100 planes
-    if (a.z0_count && (a.z0_split == 0 || a.z0_first + a.z0_split * a.z0_count > 10u)) return hipErrorInvalidValue;
+    // every part non-empty and within the 10 rows (a shorter last part when z0_limit cuts it)
+    if (a.z0_count) {
+        const uint32_t lim = a.z0_limit ? a.z0_limit : 10u;
+        if (a.z0_split == 0 || lim > 10u || a.z0_first + (a.z0_split - 1u) * a.z0_count >= lim) return hipErrorInvalidValue;
+    }
     const uint64_t grid = (uint64_t)a.njobs * (a.z0_count ? a.z0_split : 1u);
     if (grid > 0x7fffffffu) return hipErrorInvalidValue;
     if (masked)

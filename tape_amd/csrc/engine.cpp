@@ -58,9 +58,10 @@ const uint32_t g_enc_split = [] {
 // Measurement option TEC_DEBUG_KNOBS=1 TEC_ENC_SPLIT_BATCH=1: every call split that way (the seven
 // level-1 workgroups of a stripe run side by side on one XCD, so a row one of them reads as its
 // own and another as a partner is read twice at about the same time).
-const bool g_enc_split_batch = [] {
+const uint32_t g_enc_split_batch = [] {  // 0 off, else the level-1 rows per workgroup (1..7)
     const char *e = tec_knob("TEC_ENC_SPLIT_BATCH");
-    return e && e[0] == '1';
+    const int v = e ? atoi(e) : 0;
+    return (uint32_t)(v < 0 ? 0 : v > 7 ? 7 : v);
 }();
 const uint32_t g_enc_small = [] {
     const char *e = tec_knob("TEC_ENC_SMALL");
@@ -1085,8 +1086,11 @@ int encode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_data, 
             a.slice_len = (uint32_t)L.key.slice_len;
             a.n = (uint32_t)n;
             if ((per_call && total_stripes <= g_enc_split) || g_enc_split_batch) {
-                a.z0_first = 0; a.z0_count = 1; a.z0_split = 7;   // level-1 rows z0 = 0..6, one workgroup each
+                // level-1 rows z0 = 0..6: one workgroup each (or g_enc_split_batch rows each)
+                const uint32_t per = per_call ? 1u : g_enc_split_batch;
+                a.z0_first = 0; a.z0_count = per; a.z0_split = (7 + per - 1) / per; a.z0_limit = 7;
                 TE_HIP(launch_encode_dma(L.key.masked, a, s));
+                a.z0_limit = 0;
                 a.z0_first = 7; a.z0_count = 3; a.z0_split = 1;   // level 2 reads their parity back:
                 level2.push_back({L.key.masked, a});              // after every level-1 launch
             } else {

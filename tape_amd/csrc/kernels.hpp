@@ -50,6 +50,7 @@ struct EncArgs {
     // independent of each other, so a small call runs them on 7 workgroups per stripe and the
     // level-2 rows (7..9, a chain) in a second launch.
     uint32_t z0_first, z0_count, z0_split;
+    uint32_t z0_limit;     // a part's rows end at min(its start + z0_count, z0_limit) (0: no bound)
 };
 
 // Metadata suffix writer: one 48-byte record per object, copied to its n slices.
