@@ -272,10 +272,15 @@ def rank_share(args, world: int) -> tuple[int, int]:
     return args.objects, args.objects
 
 
+def coll_dev(dist, dev):
+    """Where the timing collectives' tensors live: the GPU under RCCL, the host under gloo."""
+    return dev if str(dist.get_backend()) == "nccl" else "cpu"
+
+
 def max_over_ranks(torch, dist, world: int, seconds: float, dev) -> float:
     if world <= 1:
         return seconds
-    t = torch.tensor([seconds], dtype=torch.float64, device=dev)
+    t = torch.tensor([seconds], dtype=torch.float64, device=coll_dev(dist, dev))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -344,7 +349,12 @@ def main():
     import tape_amd as T
     from tape_amd import batch
 
-    world, rank, local = dist_setup(torch, dist, "nccl")
+    # TEC_BENCH_SHARED_GPU=1 (testing the N > 1 paths on a one-GPU box): every rank on cuda:0, the
+    # timings exchanged over gloo -- RCCL refuses two ranks on one device
+    shared = os.environ.get("TEC_BENCH_SHARED_GPU") == "1"
+    world, rank, local = dist_setup(torch, dist, "gloo" if shared else "nccl")
+    if shared:
+        local = 0
     if args.workload == "config5":
         if args.mode != "encode":
             raise SystemExit("--workload config5 is an encode workload")
@@ -728,7 +738,7 @@ def gather_floats(torch, dist, world: int, x: float, dev) -> list:
     """Every rank's value of x (all_gather over the process group; only timings and flags travel)."""
     if world <= 1:
         return [x]
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64, device=coll_dev(dist, dev))
     out = [torch.zeros_like(t) for _ in range(world)]
     dist.all_gather(out, t)
     return [float(o.item()) for o in out]
