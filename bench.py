@@ -205,7 +205,19 @@ def launch_ranks(n: int, argv: list) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TEC_BENCH_LAUNCHED="1")
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE, text=True, bufsize=1))
+    # the ranks' stdout: only the JSON line goes to ours; anything else a library prints there
+    # (gloo's connection notes, ...) goes to stderr, so the driver reads exactly one line
+    import threading
+
+    def pump(p):
+        for line in p.stdout:
+            (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+            (sys.stdout if line.startswith("{") else sys.stderr).flush()
+    pumps = [threading.Thread(target=pump, args=(p,), daemon=True) for p in procs]
+    for t in pumps:
+        t.start()
     rc = 0
     pending = list(procs)
     while pending:
@@ -221,6 +233,8 @@ def launch_ranks(n: int, argv: list) -> int:
                 for q in pending:
                     q.send_signal(signal.SIGTERM)
         time.sleep(0.05)
+    for t in pumps:
+        t.join(timeout=10)
     return rc
 
 
