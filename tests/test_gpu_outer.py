@@ -19,7 +19,11 @@ def make_data(n):  # outer.rs:206-208
     return bytes(i % 251 for i in range(n))
 
 
-@pytest.mark.parametrize("k,n", [(17, 50), (7, 50), (4, 6), (10, 14), (32, 64), (40, 49), (3, 8), (1, 2)])
+# matrix kernel shapes (rs16_matrix_kernel, image <= 80 KB, k <= 32): 4-row groups G odd / even,
+# input slots KB = 16 / 32, G at its cap of 16 (5, 69), a high-rate shape (20, 40); transform
+# kernels for the rest: (32, 64) and (40, 49) exceed the image budget
+@pytest.mark.parametrize("k,n", [(17, 50), (7, 50), (4, 6), (10, 14), (32, 64), (40, 49), (3, 8), (1, 2),
+                                 (16, 48), (20, 40), (5, 69), (31, 40)])
 @pytest.mark.parametrize("size", [1, 1000, 100_003])
 def test_encode_matches_oracle(k, n, size):
     data = np.random.default_rng(k * 1000 + n + size).bytes(size)
@@ -39,7 +43,7 @@ def test_encode_max_chunk_matches_oracle():
         OuterCoder(k, n).encode(bytes(k * 4 * 1024 * 1024 + 1))  # outer.rs:82-84 TooMuchData
 
 
-@pytest.mark.parametrize("k,n", [(17, 50), (7, 50), (10, 14), (32, 64)])
+@pytest.mark.parametrize("k,n", [(17, 50), (7, 50), (10, 14), (32, 64), (16, 48), (5, 69), (31, 40)])
 def test_decode_patterns(k, n):
     rnd = random.Random(k + n)
     c = OuterCoder(k, n)
