@@ -294,11 +294,27 @@ struct Rs16MatArgs {
     uint64_t in_stride, out_stride, seg_in, seg_out;
     const uint8_t *ptr[kRs16DecPtrs];  // ptrs == 1: segment g's k inputs then rows outputs at ptr[g * (k + rows) + j]
     const uint16_t *tab;
+    const uint32_t *ktab;  // set by the launcher: rs16_mat_tailv's constants (after the staged image)
     uint32_t k, rows, elems, segments, ptrs;
     uint32_t rstride;  // set by the launcher: image bytes per input (a run-time value, so the kernel's
                        // per-input bases stay one scalar each instead of 4k folded constants)
 };
-inline size_t rs16_mat_bytes(uint32_t k, uint32_t rows) { return (size_t)k * ((rows + 3) / 4) * 512u; }
+// TEC_RS16_MAT_TV=1 (off by default: measured slower): for rows = 8 h + 1 (OuterCoder(17, 50):
+// 33 encode rows, 17 decode rows) the last row is computed bit-serially on the VALU from 16
+// per-input constants instead of an 8-byte table read per nibble (which serves 4 rows for the 1
+// needed), so the LDS array moves only whole 8-row entries.  r05 on the GPU: encode 1.67 ms
+// against 1.58, decode 1.36 against 1.20 -- the VALU (~70 % busy) cannot take 3 more
+// instructions per bit of every input.
+#ifndef TEC_RS16_MAT_TV
+#define TEC_RS16_MAT_TV 0
+#endif
+inline bool rs16_mat_tailv(uint32_t rows) { return TEC_RS16_MAT_TV && rows % 8 == 1 && rows > 1; }
+inline size_t rs16_mat_bytes(uint32_t k, uint32_t rows) {  // the LDS-staged part of the image
+    return rs16_mat_tailv(rows) ? (size_t)k * (rows / 8) * 1024u : (size_t)k * ((rows + 3) / 4) * 512u;
+}
+inline size_t rs16_mat_image_bytes(uint32_t k, uint32_t rows) {  // + the tail row's constants (k x 16 u32)
+    return rs16_mat_bytes(k, rows) + (rs16_mat_tailv(rows) ? (size_t)k * 64u : 0u);
+}
 inline bool rs16_mat_supported(uint32_t k, uint32_t rows) {
     return k >= 1 && k <= 32 && rows >= 1 && (rows + 3) / 4 <= kRs16MatMaxG && rs16_mat_bytes(k, rows) <= kRs16MatLds;
 }

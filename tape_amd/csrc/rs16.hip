@@ -342,9 +342,10 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 // One input's products for the thread's E elements (element e's 16 bits at bit sh + 16 e of w).
-template <int G, int E>
+// TV: no tail group in the image (rows = 8 NP + 1; mat_tail computes the last row).
+template <int G, int E, bool TV>
 __device__ __forceinline__ void mat_input(uint32_t (&acc)[E][2 * G], const uint8_t *blk, uint32_t w, int sh) {
-    constexpr int NP = G / 2;
+    constexpr int NP = G / 2, BG = TV ? 2 * NP : G;  // BG: 4-row groups per (r, q) block
     uint32_t n[E][4];
 #pragma unroll
     for (int e = 0; e < E; e++)
@@ -356,14 +357,14 @@ __device__ __forceinline__ void mat_input(uint32_t (&acc)[E][2 * G], const uint8
 #pragma unroll
         for (int e = 0; e < E; e++)
 #pragma unroll
-            for (int q = 0; q < 4; q++) v[e][q] = *(lds_u32x4 *)(blk + (n[e][q] << 4) + (q * G * 128 + h * 256));
+            for (int q = 0; q < 4; q++) v[e][q] = *(lds_u32x4 *)(blk + (n[e][q] << 4) + (q * BG * 128 + h * 256));
 #pragma unroll
         for (int e = 0; e < E; e++)
 #pragma unroll
             for (int d = 0; d < 4; d++)
                 acc[e][4 * h + d] = xor3(xor3(acc[e][4 * h + d], v[e][0][d], v[e][1][d]), v[e][2][d], v[e][3][d]);
     }
-    if constexpr (G % 2) {  // tail group: entries of 8 B at NP * 256 within each nibble block
+    if constexpr (G % 2 && !TV) {  // tail group: entries of 8 B at NP * 256 within each nibble block
         u32x2 v[E][4];
 #pragma unroll
         for (int e = 0; e < E; e++)
@@ -377,24 +378,58 @@ __device__ __forceinline__ void mat_input(uint32_t (&acc)[E][2 * G], const uint8
     }
 }
 
+// t ^ (m & c) (v_bitop3_b32, LUT over src0 = 0xf0, src1 = 0xcc, src2 = 0xaa)
+__device__ __forceinline__ uint32_t xor_and(uint32_t t, uint32_t m, uint32_t c) {
+    uint32_t d;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(d) : "v"(t), "v"(m), "s"(c));
+    return d;
+}
+// The lone last row of rows = 8 h + 1 on the VALU: x * c = XOR over the set bits b of x of K[b] =
+// c * 2^b (16 constants per input, scalar loads).  E = 2: both elements at once -- bit b of each
+// half spread over its half by a packed shift pair (v_pk_lshlrev_b16 / v_pk_ashrrev_i16), K[b]
+// in both halves: 3 VALU per bit for two products, against the tail group's 8 LDS cycles (4-row
+// entries of which 1 row is used) in the LDS-bound kernel.  Products accumulate in t (element e
+// in half e; E = 1: the low half).
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(4))) const uint32_t const_u32;  // constant space: scalar loads
+template <int E>
+__device__ __forceinline__ uint32_t mat_tail(uint32_t t, uint32_t w, int sh, const_u32 *K) {
+#pragma unroll
+    for (int b = 0; b < 16; b++) {
+        uint32_t m;
+        if constexpr (E == 2) {
+            s16x2 x = __builtin_bit_cast(s16x2, w);
+            if (b != 15) x = (s16x2)(x << (short)(15 - b));
+            m = __builtin_bit_cast(uint32_t, (s16x2)(x >> (short)15));
+        } else {
+            m = (uint32_t)__builtin_amdgcn_sbfe((int)w, sh + b, 1);
+        }
+        t = xor_and(t, m, K[b]);
+    }
+    return t;
+}
+
 #ifndef TEC_RS16_MAT_E
 #define TEC_RS16_MAT_E 2     // elements per thread: 2 (16-bit loads / stores) or 1 (byte ones, fewer VGPRs)
 #endif
 #ifndef TEC_RS16_MAT_BT
 #define TEC_RS16_MAT_BT 512  // threads per block (2 blocks per CU at OuterCoder(17, 50)'s 78 KB image)
 #endif
+#ifndef TEC_RS16_MAT_TVPOS
+#define TEC_RS16_MAT_TVPOS 1  // where the VALU tail row runs: 1 = before the table reads, 0 = per input beside them
+#endif
 #ifndef TEC_RS16_MAT_WPE
 #define TEC_RS16_MAT_WPE 4   // waves per SIMD the registers are budgeted for
 #endif
 constexpr int kMatE = TEC_RS16_MAT_E, kMatBT = TEC_RS16_MAT_BT;
 
-template <int G, int KB, bool PTRS>  // KB: input slots (k <= KB)
+template <int G, int KB, bool PTRS, bool TV>  // KB: input slots (k <= KB); TV: rows = 8 (G / 2) + 1, mat_tail
 __global__ void __launch_bounds__(kMatBT) __attribute__((amdgpu_waves_per_eu(TEC_RS16_MAT_WPE)))
 rs16_matrix_kernel(Rs16MatArgs a) {
-    constexpr int E = kMatE;
+    constexpr int E = kMatE, NP = G / 2, BG = TV ? 2 * NP : G;
     extern __shared__ __attribute__((aligned(16))) uint16_t lds16[];
     {
-        const uint32_t n16 = a.k * (uint32_t)G * 32u;  // 16-byte units of the image
+        const uint32_t n16 = a.k * (uint32_t)BG * 32u;  // 16-byte units of the image
         for (uint32_t t = threadIdx.x; t < n16; t += blockDim.x)
             reinterpret_cast<uint4 *>(lds16)[t] = reinterpret_cast<const uint4 *>(a.tab)[t];
     }
@@ -408,7 +443,8 @@ rs16_matrix_kernel(Rs16MatArgs a) {
         // spilled to VGPR lanes); a few scalar ops per tile instead
         uint32_t k = a.k, rstride = a.rstride;
         uint64_t in_stride = a.in_stride, out_stride = a.out_stride;
-        asm volatile("" : "+s"(k), "+s"(rstride), "+s"(in_stride), "+s"(out_stride));
+        const uint32_t *ktab = a.ktab;
+        asm volatile("" : "+s"(k), "+s"(rstride), "+s"(in_stride), "+s"(out_stride), "+s"(ktab));
         const uint32_t seg = tile / tps, u = (tile - seg * tps) * blockDim.x + threadIdx.x;
         if (u >= units) continue;
         const uint32_t e0 = E * u, eo = (e0 >> 5) * 64u + (e0 & 31u);
@@ -442,9 +478,27 @@ rs16_matrix_kernel(Rs16MatArgs a) {
         }
 #pragma unroll
         for (int j = 0; j < NW; j++) asm volatile("" ::"v"(P[j]));
+        // TV: the tail products first, in their own pass (TEC_RS16_MAT_TVPOS 1): their scalar
+        // loads share lgkmcnt with the LDS reads and return out of order, so each use waits for
+        // lgkmcnt(0) -- interleaved with the table reads (0) that drains the wave's LDS queue per input
+        uint32_t tv = 0;
+        if constexpr (TV && TEC_RS16_MAT_TVPOS == 1) {
+#pragma unroll
+            for (int r = 0; r < KB; r++)
+                if ((uint32_t)r < k) tv = mat_tail<E>(tv, E == 2 ? P[r] : P[r >> 1], E == 2 ? 0 : 16 * (r & 1), (const_u32 *)ktab + r * 16);
+        }
 #pragma unroll
         for (int r = 0; r < KB; r++)
-            if ((uint32_t)r < k) mat_input<G, E>(acc, tab + r * rstride, E == 2 ? P[r] : P[r >> 1], E == 2 ? 0 : 16 * (r & 1));
+            if ((uint32_t)r < k) {
+                const uint32_t w = E == 2 ? P[r] : P[r >> 1];
+                const int sh = E == 2 ? 0 : 16 * (r & 1);
+                mat_input<G, E, TV>(acc, tab + r * rstride, w, sh);
+                if constexpr (TV && TEC_RS16_MAT_TVPOS == 0) tv = mat_tail<E>(tv, w, sh, (const_u32 *)ktab + r * 16);
+            }
+        if constexpr (TV) {
+            acc[0][4 * NP] = tv & 0xffffu;
+            if constexpr (E == 2) acc[E - 1][4 * NP] = tv >> 16;
+        }
 #pragma unroll
         for (int i = 0; i < 4 * G; i++) {
             if ((uint32_t)i >= a.rows) continue;
@@ -464,15 +518,22 @@ rs16_matrix_kernel(Rs16MatArgs a) {
     }
 }
 
-template <int G, int KB>
-hipError_t launch_mat_gk(Rs16MatArgs a, uint32_t grid, size_t lds, hipStream_t s) {
-    a.rstride = 4u * G * 128u;
-    const void *fn = a.ptrs ? reinterpret_cast<const void *>(rs16_matrix_kernel<G, KB, true>)
-                            : reinterpret_cast<const void *>(rs16_matrix_kernel<G, KB, false>);
+template <int G, int KB, bool TV>
+hipError_t launch_mat_gkt(Rs16MatArgs a, uint32_t grid, size_t lds, hipStream_t s) {
+    a.rstride = 4u * (TV ? G - 1 : G) * 128u;
+    a.ktab = TV ? reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(a.tab) + lds) : nullptr;
+    const void *fn = a.ptrs ? reinterpret_cast<const void *>(rs16_matrix_kernel<G, KB, true, TV>)
+                            : reinterpret_cast<const void *>(rs16_matrix_kernel<G, KB, false, TV>);
     if (const hipError_t e = ensure_dyn_lds(fn, lds); e != hipSuccess) return e;
-    if (a.ptrs) hipLaunchKernelGGL((rs16_matrix_kernel<G, KB, true>), dim3(grid), dim3(kMatBT), lds, s, a);
-    else hipLaunchKernelGGL((rs16_matrix_kernel<G, KB, false>), dim3(grid), dim3(kMatBT), lds, s, a);
+    if (a.ptrs) hipLaunchKernelGGL((rs16_matrix_kernel<G, KB, true, TV>), dim3(grid), dim3(kMatBT), lds, s, a);
+    else hipLaunchKernelGGL((rs16_matrix_kernel<G, KB, false, TV>), dim3(grid), dim3(kMatBT), lds, s, a);
     return hipGetLastError();
+}
+template <int G, int KB>
+hipError_t launch_mat_gk(const Rs16MatArgs &a, uint32_t grid, size_t lds, hipStream_t s) {
+    if constexpr (TEC_RS16_MAT_TV && G % 2 == 1 && G > 1)
+        if (rs16_mat_tailv(a.rows)) return launch_mat_gkt<G, KB, true>(a, grid, lds, s);
+    return launch_mat_gkt<G, KB, false>(a, grid, lds, s);
 }
 template <int G>
 hipError_t launch_mat_g(const Rs16MatArgs &a, uint32_t grid, size_t lds, hipStream_t s) {

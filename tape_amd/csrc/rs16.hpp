@@ -216,14 +216,27 @@ inline void encode_matrix(uint32_t k, uint32_t m, std::vector<uint16_t> &E) {
 // products M[row][r] * (n << 4q) -- groups 2h and 2h + 1 (8 rows) as 16 entries of 8 u16 at h * 128
 // + n * 8, and for odd G the last group as 16 entries of 4 u16 at (G / 2) * 128 + n * 4.  Zero past
 // the last row.
-inline std::vector<uint16_t> mat_image(uint32_t k, uint32_t rows, const uint16_t *M) {
+// tv (rows = 8 h + 1, kernels.hpp rs16_mat_tailv): the last row is not in the blocks (h x 128
+// u16 per (r, q)); after them, per input r 16 u32 constants K[r][b] = M[rows - 1][r] * (1 << b),
+// the product in both halves (the product is linear over GF(2): x * c = XOR of K[b] over the set
+// bits b of x; the kernel applies it to two elements at once).
+inline std::vector<uint16_t> mat_image(uint32_t k, uint32_t rows, const uint16_t *M, bool tv = false) {
     const Tables &T = tables();
+    tv = tv && rows % 8 == 1 && rows > 1;
     const uint32_t G = (rows + 3) / 4, NP = G / 2;
-    std::vector<uint16_t> img((size_t)k * 4 * G * 64, 0);
+    const uint32_t BG = tv ? 2 * NP : G;  // 4-row groups per (r, q) block in LDS
+    std::vector<uint16_t> img((size_t)k * 4 * BG * 64 + (tv ? (size_t)k * 32 : 0), 0);
+    if (tv) {
+        uint16_t *kt = img.data() + (size_t)k * 4 * BG * 64;
+        for (uint32_t r = 0; r < k; r++)
+            for (uint32_t b = 0; b < 16; b++)
+                kt[((size_t)r * 16 + b) * 2] = kt[((size_t)r * 16 + b) * 2 + 1] =
+                    T.gmul((uint16_t)(1u << b), M[(size_t)(rows - 1) * k + r]);
+    }
     for (uint32_t r = 0; r < k; r++)
         for (uint32_t q = 0; q < 4; q++) {
-            uint16_t *blk = img.data() + ((size_t)r * 4 + q) * G * 64;
-            for (uint32_t row = 0; row < rows; row++) {
+            uint16_t *blk = img.data() + ((size_t)r * 4 + q) * BG * 64;
+            for (uint32_t row = 0; row < (tv ? rows - 1 : rows); row++) {
                 const uint32_t g = row / 4, j = row % 4;
                 const uint16_t c = M[(size_t)row * k + r];
                 for (uint32_t n = 0; n < 16; n++) {
