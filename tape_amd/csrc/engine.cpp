@@ -3364,6 +3364,39 @@ int te_clay_encode(te_clay *c, const uint8_t *data, size_t len, uint8_t *chunks,
     return TE_OK;
 }
 
+}  // extern "C"
+// The given slices (n pointers, null = absent) to c->io_in at i * len, on c->stream.  Page-locked
+// ones are copied directly; short pageable ones are first gathered into the handle's pinned
+// staging by the copy pool: each pageable H2D goes through the driver's staging at ~57 us of
+// fixed cost (te_slicer_decode, 7 x 715 KB: 1.11 -> 0.81 ms per 4 MiB call, against 0.70 with
+// pinned slices, r05).  Long ones go to the driver, whose pageable path outruns the 4-thread
+// memcpy there (7 x 11.4 MB, 64 MiB object: 3.03 ms direct, 4.2-4.5 gathered).
+constexpr size_t kGatherMaxSlice = 2u << 20;
+static int upload_slices(te_clay *c, const uint8_t *const *slices, size_t len) {
+    const int n = c->h.n;
+    bool direct = true;  // every slice page-locked, or long
+    int given = 0;
+    for (int i = 0; i < n; i++)
+        if (slices[i]) given++, direct = direct && (len > kGatherMaxSlice || host_pinned(slices[i]));
+    const uint8_t *src[64];
+    if (!direct) {
+        TE_HIP(c->hio_in.ensure((size_t)given * len));
+        std::vector<CopyPool::Seg> segs;
+        for (int i = 0, g = 0; i < n; i++)
+            if (slices[i]) {
+                src[i] = c->hio_in.u8() + (size_t)g++ * len;
+                segs.push_back({const_cast<uint8_t *>(src[i]), slices[i], len});
+            }
+        CopyPool::get().run(segs);
+    }
+    for (int i = 0; i < n; i++)
+        if (slices[i])
+            TE_HIP(hipMemcpyAsync(c->io_in.as<uint8_t>() + (size_t)i * len, direct ? slices[i] : src[i], len,
+                                  hipMemcpyHostToDevice, c->stream));
+    return TE_OK;
+}
+extern "C" {
+
 int te_clay_decode(te_clay *c, const uint8_t *const *chunks, size_t cs, uint8_t *out, size_t cap) {
     if (!c || !chunks || !out) return TE_ERR_INVALID_ARG;
     const ClayHost &h = c->h;
@@ -3382,9 +3415,8 @@ int te_clay_decode(te_clay *c, const uint8_t *const *chunks, size_t cs, uint8_t 
     const size_t total = (size_t)h.n * cs;
     TE_HIP(c->io_in.ensure(total));
     TE_HIP(c->io_out.ensure((size_t)h.k * cs));
-    for (int i = 0; i < h.n; i++)
-        if (chunks[i])
-            TE_HIP(hipMemcpyAsync(c->io_in.as<uint8_t>() + (size_t)i * cs, chunks[i], cs, hipMemcpyHostToDevice, c->stream));
+    r = upload_slices(c, chunks, cs);
+    if (r) return r;
     DecItem it{};
     it.in_base = 0; it.slice_len = cs; it.blob_len = (uint64_t)h.k * cs; it.stripe = it.blob_len; it.ns = 1; it.cs = cs;
     it.out_off = 0; it.avail = avail;
@@ -3419,10 +3451,8 @@ int te_slicer_decode(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *const 
     const size_t total = (size_t)h.n * slice_len;
     TE_HIP(c->io_in.ensure(total));
     TE_HIP(c->io_out.ensure(it.blob_len));
-    for (int i = 0; i < h.n; i++)
-        if (slices[i])
-            TE_HIP(hipMemcpyAsync(c->io_in.as<uint8_t>() + (size_t)i * slice_len, slices[i], slice_len,
-                                  hipMemcpyHostToDevice, c->stream));
+    r = upload_slices(c, slices, slice_len);
+    if (r) return r;
     it.in_base = 0;
     it.out_off = 0;
     r = decode_enqueue(c, cfg, c->io_in.as<uint8_t>(), &it, 1, c->io_out.as<uint8_t>(), c->stream, false);
