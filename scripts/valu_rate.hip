@@ -7,11 +7,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 constexpr int kIter = 4096;
 
 template <int OP>
-__device__ __forceinline__ void op(uint32_t &a, uint32_t b, uint32_t c, uint32_t s) {
+__device__ __forceinline__ void op(uint32_t &a, uint32_t b, uint32_t c, uint32_t &s) {
     if constexpr (OP == 0) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a) : "v"(b));
     if constexpr (OP == 1) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a) : "v"(b), "v"(c));
     if constexpr (OP == 2) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x78" : "+v"(a) : "v"(b), "s"(s));
@@ -19,12 +20,18 @@ __device__ __forceinline__ void op(uint32_t &a, uint32_t b, uint32_t c, uint32_t
     if constexpr (OP == 4) asm volatile("v_pk_lshlrev_b16 %0, 3, %0 op_sel_hi:[0,1]" : "+v"(a));
     if constexpr (OP == 5) asm volatile("v_bfe_u32 %0, %0, %1, 4" : "+v"(a) : "v"(b));
     if constexpr (OP == 6) asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(a) : "v"(b));
+    if constexpr (OP == 7) asm volatile("v_and_b32_e32 %0, 0x7f7f7f7f, %0" : "+v"(a));  // VOP2 + 32-bit literal (8 bytes)
+    if constexpr (OP == 8) asm volatile("v_xor_b32_e64 %0, %0, %1" : "+v"(a) : "v"(b));  // VOP2 op in the VOP3 encoding
+    if constexpr (OP == 9) asm volatile("v_xor_b32_e32 %0, %1, %0" : "+v"(a) : "s"(s));  // VOP2, SGPR operand
+    if constexpr (OP == 10) asm volatile("v_mul_u32_u24_e32 %0, %1, %0" : "+v"(a) : "v"(b));
+    if constexpr (OP == 11) asm volatile("v_readlane_b32 %0, %1, 5" : "=s"(s) : "v"(a));
 }
 
 template <int OP>
 __global__ void __launch_bounds__(256) rate_kernel(uint32_t *out, uint32_t seed, uint64_t *cyc) {
     uint32_t a[8];
-    const uint32_t b = seed ^ threadIdx.x, c = seed * 3u + threadIdx.x, s = seed * 5u;
+    const uint32_t b = seed ^ threadIdx.x, c = seed * 3u + threadIdx.x;
+    uint32_t s = seed * 5u;
 #pragma unroll
     for (int i = 0; i < 8; i++) a[i] = threadIdx.x * (i + 1);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
@@ -38,6 +45,7 @@ __global__ void __launch_bounds__(256) rate_kernel(uint32_t *out, uint32_t seed,
     uint32_t x = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) x ^= a[i];
+    x ^= s;
     out[blockIdx.x * blockDim.x + threadIdx.x] = x;
     if (threadIdx.x == 0 && blockIdx.x == 0) *cyc = t1 - t0;
 }
@@ -72,6 +80,18 @@ int main() {
     int clk = 0;
     (void)hipDeviceGetAttribute(&clk, hipDeviceAttributeClockRate, 0);
     printf("clock attribute %d kHz\n", clk);
+    if (getenv("VALU_RATE_EXTRA")) {  // encodings: literal, VOP3-encoded VOP2, SGPR operand, readlane
+        for (int W : {4, 8}) {
+            run<0>("v_xor_b32", W, d_out, d_cyc);
+            run<7>("v_and_b32 literal", W, d_out, d_cyc);
+            run<8>("v_xor_b32_e64", W, d_out, d_cyc);
+            run<9>("v_xor_b32 sgpr", W, d_out, d_cyc);
+            run<10>("v_mul_u32_u24", W, d_out, d_cyc);
+            run<11>("v_readlane_b32", W, d_out, d_cyc);
+            run<1>("v_bitop3 vvv", W, d_out, d_cyc);
+        }
+        return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+    }
     for (int W : {1, 2, 4, 8}) {
         run<0>("v_xor_b32", W, d_out, d_cyc);
         run<1>("v_bitop3 vvv", W, d_out, d_cyc);
