@@ -2,7 +2,7 @@
 # round-5 closing check: whole GPU suite, smoke, and the bench lines (default, modes, outer, percall)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/final_r05
+O=gpurun_out/${FINAL_DIR:-final_r05}
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
 tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
