@@ -162,8 +162,13 @@ static void compile(DecJit *j, Entry *E, std::string src, size_t lds, uint32_t n
     if (hiprtcCreateProgram(&prog, src.c_str(), "tec_dec_fixed.hip", 1, hdrs, names) != HIPRTC_SUCCESS) {
         err = "hiprtcCreateProgram failed";
     } else {
-        const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-        if (hiprtcCompileProgram(prog, 3, opts) != HIPRTC_SUCCESS) {
+        // TEC_DEC_JIT_SCHED (measurement): the backend scheduling strategy, e.g. max-ilp
+        static const std::string sched = [] {
+            const char *e = tec_knob("TEC_DEC_JIT_SCHED");
+            return e ? std::string("-amdgpu-sched-strategy=") + e : std::string();
+        }();
+        const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-mllvm", sched.c_str()};
+        if (hiprtcCompileProgram(prog, sched.empty() ? 3 : 5, opts) != HIPRTC_SUCCESS) {
             size_t n = 0;
             hiprtcGetProgramLogSize(prog, &n);
             std::string log(n, '\0');
