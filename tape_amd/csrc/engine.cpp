@@ -3974,7 +3974,7 @@ int outer_lut(uint32_t k, uint32_t m, const std::vector<uint32_t> &recv, const s
         std::vector<uint16_t> Dm((size_t)rows * k);
         for (uint32_t i = 0; i < rows; i++)
             memcpy(&Dm[(size_t)i * k], &D[(size_t)(enc ? i : miss[i]) * k], k * sizeof(uint16_t));
-        lut = rs16::mat_image(k, rows, Dm.data(), rs16_mat_tailv(rows));
+        lut = rs16::mat_image(k, rows, Dm.data(), rs16_mat_tailv(rows), rs16_mat_tail_bytes(rows));
     } else {
         const rs16::Tables &T = rs16::tables();
         lut.assign((size_t)nm * k * 64, 0);

@@ -309,8 +309,23 @@ struct Rs16MatArgs {
 #define TEC_RS16_MAT_TV 0
 #endif
 inline bool rs16_mat_tailv(uint32_t rows) { return TEC_RS16_MAT_TV && rows % 8 == 1 && rows > 1; }
+// The odd last 4-row group (G = ceil(rows / 4) odd) holds rows - 8 (G / 2) rows: its nibble
+// entries are 2 B for one row (ds_read_u16), 4 B for two (ds_read_b32), else 8 B (ds_read_b64) --
+// TEC_RS16_MAT_NARROW=0: 8 B always.  The LDS array bounds the kernel, and an 8-byte
+// read serving one row's products was a quarter used.
+#ifndef TEC_RS16_MAT_NARROW
+#define TEC_RS16_MAT_NARROW 1
+#endif
+inline uint32_t rs16_mat_tail_bytes(uint32_t rows) {
+    const uint32_t G = (rows + 3) / 4;
+    if (!(G & 1) || rs16_mat_tailv(rows)) return 0;
+    const uint32_t t = rows - 8 * (G / 2);
+    return !TEC_RS16_MAT_NARROW || t > 2 ? 8u : 2u * t;
+}
+// bytes of one (input, nibble position) block: G / 2 pair tables of 256 B, then the tail table
+inline uint32_t rs16_mat_block_bytes(uint32_t rows) { return ((rows + 3) / 4 / 2) * 256u + 16u * rs16_mat_tail_bytes(rows); }
 inline size_t rs16_mat_bytes(uint32_t k, uint32_t rows) {  // the LDS-staged part of the image
-    return rs16_mat_tailv(rows) ? (size_t)k * (rows / 8) * 1024u : (size_t)k * ((rows + 3) / 4) * 512u;
+    return (size_t)k * 4u * rs16_mat_block_bytes(rows);
 }
 inline size_t rs16_mat_image_bytes(uint32_t k, uint32_t rows) {  // + the tail row's constants (k x 16 u32)
     return rs16_mat_bytes(k, rows) + (rs16_mat_tailv(rows) ? (size_t)k * 64u : 0u);

@@ -342,10 +342,16 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 // One input's products for the thread's E elements (element e's 16 bits at bit sh + 16 e of w).
-// TV: no tail group in the image (rows = 8 NP + 1; mat_tail computes the last row).
-template <int G, int E, bool TV>
+// TV: no tail group in the image (rows = 8 NP + 1; mat_tail computes the last row).  TB: the tail
+// group's entry bytes (kernels.hpp rs16_mat_tail_bytes): 2 = one row (ds_read_u16, 1 LDS cycle
+// instead of the 8-byte read's 2), 4 = two rows (ds_read_b32), 8 = three or four.
+typedef __attribute__((address_space(3))) const uint16_t lds_u16;
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+template <int G, int TB, bool TV>
+constexpr int mat_block_bytes() { return (G / 2) * 256 + ((G % 2 && !TV) ? 16 * TB : 0); }
+template <int G, int E, bool TV, int TB>
 __device__ __forceinline__ void mat_input(uint32_t (&acc)[E][2 * G], const uint8_t *blk, uint32_t w, int sh) {
-    constexpr int NP = G / 2, BG = TV ? 2 * NP : G;  // BG: 4-row groups per (r, q) block
+    constexpr int NP = G / 2, BQ = mat_block_bytes<G, TB, TV>();  // BQ: bytes per (r, q) block
     uint32_t n[E][4];
 #pragma unroll
     for (int e = 0; e < E; e++)
@@ -357,24 +363,37 @@ __device__ __forceinline__ void mat_input(uint32_t (&acc)[E][2 * G], const uint8
 #pragma unroll
         for (int e = 0; e < E; e++)
 #pragma unroll
-            for (int q = 0; q < 4; q++) v[e][q] = *(lds_u32x4 *)(blk + (n[e][q] << 4) + (q * BG * 128 + h * 256));
+            for (int q = 0; q < 4; q++) v[e][q] = *(lds_u32x4 *)(blk + (n[e][q] << 4) + (q * BQ + h * 256));
 #pragma unroll
         for (int e = 0; e < E; e++)
 #pragma unroll
             for (int d = 0; d < 4; d++)
                 acc[e][4 * h + d] = xor3(xor3(acc[e][4 * h + d], v[e][0][d], v[e][1][d]), v[e][2][d], v[e][3][d]);
     }
-    if constexpr (G % 2 && !TV) {  // tail group: entries of 8 B at NP * 256 within each nibble block
+    if constexpr (G % 2 && !TV && TB == 8) {  // tail group: entries of 8 B at NP * 256 within each nibble block
         u32x2 v[E][4];
 #pragma unroll
         for (int e = 0; e < E; e++)
 #pragma unroll
-            for (int q = 0; q < 4; q++) v[e][q] = *(lds_u32x2 *)(blk + (n[e][q] << 3) + (q * G * 128 + NP * 256));
+            for (int q = 0; q < 4; q++) v[e][q] = *(lds_u32x2 *)(blk + (n[e][q] << 3) + (q * BQ + NP * 256));
 #pragma unroll
         for (int e = 0; e < E; e++)
 #pragma unroll
             for (int d = 0; d < 2; d++)
                 acc[e][4 * NP + d] = xor3(xor3(acc[e][4 * NP + d], v[e][0][d], v[e][1][d]), v[e][2][d], v[e][3][d]);
+    } else if constexpr (G % 2 && !TV) {  // 2- or 4-byte entries: rows 8 NP (+ 1) in acc[e][4 NP]
+        uint32_t v[E][4];
+#pragma unroll
+        for (int e = 0; e < E; e++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint8_t *at = blk + n[e][q] * TB + (q * BQ + NP * 256);
+                if constexpr (TB == 2) v[e][q] = *(lds_u16 *)at;
+                else v[e][q] = *(lds_u32 *)at;
+            }
+#pragma unroll
+        for (int e = 0; e < E; e++)
+            acc[e][4 * NP] = xor3(xor3(acc[e][4 * NP], v[e][0], v[e][1]), v[e][2], v[e][3]);
     }
 }
 
@@ -423,13 +442,13 @@ __device__ __forceinline__ uint32_t mat_tail(uint32_t t, uint32_t w, int sh, con
 #endif
 constexpr int kMatE = TEC_RS16_MAT_E, kMatBT = TEC_RS16_MAT_BT;
 
-template <int G, int KB, bool PTRS, bool TV>  // KB: input slots (k <= KB); TV: rows = 8 (G / 2) + 1, mat_tail
+template <int G, int KB, bool PTRS, bool TV, int TB>  // KB: input slots (k <= KB); TV: rows = 8 (G / 2) + 1, mat_tail; TB: tail entry bytes
 __global__ void __launch_bounds__(kMatBT) __attribute__((amdgpu_waves_per_eu(TEC_RS16_MAT_WPE)))
 rs16_matrix_kernel(Rs16MatArgs a) {
-    constexpr int E = kMatE, NP = G / 2, BG = TV ? 2 * NP : G;
+    constexpr int E = kMatE, NP = G / 2, BQ = mat_block_bytes<G, TB, TV>();
     extern __shared__ __attribute__((aligned(16))) uint16_t lds16[];
     {
-        const uint32_t n16 = a.k * (uint32_t)BG * 32u;  // 16-byte units of the image
+        const uint32_t n16 = a.k * (uint32_t)BQ / 4u;  // 16-byte units of the image (4 blocks per input)
         for (uint32_t t = threadIdx.x; t < n16; t += blockDim.x)
             reinterpret_cast<uint4 *>(lds16)[t] = reinterpret_cast<const uint4 *>(a.tab)[t];
     }
@@ -492,7 +511,7 @@ rs16_matrix_kernel(Rs16MatArgs a) {
             if ((uint32_t)r < k) {
                 const uint32_t w = E == 2 ? P[r] : P[r >> 1];
                 const int sh = E == 2 ? 0 : 16 * (r & 1);
-                mat_input<G, E, TV>(acc, tab + r * rstride, w, sh);
+                mat_input<G, E, TV, TB>(acc, tab + r * rstride, w, sh);
                 if constexpr (TV && TEC_RS16_MAT_TVPOS == 0) tv = mat_tail<E>(tv, w, sh, (const_u32 *)ktab + r * 16);
             }
         if constexpr (TV) {
@@ -518,22 +537,30 @@ rs16_matrix_kernel(Rs16MatArgs a) {
     }
 }
 
-template <int G, int KB, bool TV>
+template <int G, int KB, bool TV, int TB>
 hipError_t launch_mat_gkt(Rs16MatArgs a, uint32_t grid, size_t lds, hipStream_t s) {
-    a.rstride = 4u * (TV ? G - 1 : G) * 128u;
+    a.rstride = 4u * (uint32_t)mat_block_bytes<G, TB, TV>();
+    if ((size_t)a.k * a.rstride != lds) return hipErrorInvalidValue;  // host image and kernel layout agree
     a.ktab = TV ? reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(a.tab) + lds) : nullptr;
-    const void *fn = a.ptrs ? reinterpret_cast<const void *>(rs16_matrix_kernel<G, KB, true, TV>)
-                            : reinterpret_cast<const void *>(rs16_matrix_kernel<G, KB, false, TV>);
+    const void *fn = a.ptrs ? reinterpret_cast<const void *>(rs16_matrix_kernel<G, KB, true, TV, TB>)
+                            : reinterpret_cast<const void *>(rs16_matrix_kernel<G, KB, false, TV, TB>);
     if (const hipError_t e = ensure_dyn_lds(fn, lds); e != hipSuccess) return e;
-    if (a.ptrs) hipLaunchKernelGGL((rs16_matrix_kernel<G, KB, true, TV>), dim3(grid), dim3(kMatBT), lds, s, a);
-    else hipLaunchKernelGGL((rs16_matrix_kernel<G, KB, false, TV>), dim3(grid), dim3(kMatBT), lds, s, a);
+    if (a.ptrs) hipLaunchKernelGGL((rs16_matrix_kernel<G, KB, true, TV, TB>), dim3(grid), dim3(kMatBT), lds, s, a);
+    else hipLaunchKernelGGL((rs16_matrix_kernel<G, KB, false, TV, TB>), dim3(grid), dim3(kMatBT), lds, s, a);
     return hipGetLastError();
 }
 template <int G, int KB>
 hipError_t launch_mat_gk(const Rs16MatArgs &a, uint32_t grid, size_t lds, hipStream_t s) {
-    if constexpr (TEC_RS16_MAT_TV && G % 2 == 1 && G > 1)
-        if (rs16_mat_tailv(a.rows)) return launch_mat_gkt<G, KB, true>(a, grid, lds, s);
-    return launch_mat_gkt<G, KB, false>(a, grid, lds, s);
+    if constexpr (G % 2 == 1) {
+        if constexpr (TEC_RS16_MAT_TV && G > 1)
+            if (rs16_mat_tailv(a.rows)) return launch_mat_gkt<G, KB, true, 8>(a, grid, lds, s);
+        switch (rs16_mat_tail_bytes(a.rows)) {
+            case 2: return launch_mat_gkt<G, KB, false, 2>(a, grid, lds, s);
+            case 4: return launch_mat_gkt<G, KB, false, 4>(a, grid, lds, s);
+            default: break;
+        }
+    }
+    return launch_mat_gkt<G, KB, false, 8>(a, grid, lds, s);
 }
 template <int G>
 hipError_t launch_mat_g(const Rs16MatArgs &a, uint32_t grid, size_t lds, hipStream_t s) {

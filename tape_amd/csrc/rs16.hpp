@@ -220,14 +220,19 @@ inline void encode_matrix(uint32_t k, uint32_t m, std::vector<uint16_t> &E) {
 // u16 per (r, q)); after them, per input r 16 u32 constants K[r][b] = M[rows - 1][r] * (1 << b),
 // the product in both halves (the product is linear over GF(2): x * c = XOR of K[b] over the set
 // bits b of x; the kernel applies it to two elements at once).
-inline std::vector<uint16_t> mat_image(uint32_t k, uint32_t rows, const uint16_t *M, bool tv = false) {
+// tail_bytes (kernels.hpp rs16_mat_tail_bytes, odd G only): the last group's entry size, 2 / 4 / 8 B
+// for 1 / 2 / 3-4 rows (16 entries of tail_bytes at (G / 2) * 128 u16); the block of (r, q) is
+// (G / 2) * 128 + 8 * tail_bytes u16.
+inline std::vector<uint16_t> mat_image(uint32_t k, uint32_t rows, const uint16_t *M, bool tv = false,
+                                       uint32_t tail_bytes = 8) {
     const Tables &T = tables();
     tv = tv && rows % 8 == 1 && rows > 1;
     const uint32_t G = (rows + 3) / 4, NP = G / 2;
-    const uint32_t BG = tv ? 2 * NP : G;  // 4-row groups per (r, q) block in LDS
-    std::vector<uint16_t> img((size_t)k * 4 * BG * 64 + (tv ? (size_t)k * 32 : 0), 0);
+    const uint32_t TBu = (G % 2 && !tv) ? tail_bytes / 2 : 0;  // u16 per tail entry
+    const uint32_t BQ = NP * 128 + 16 * TBu;                   // u16 per (r, q) block
+    std::vector<uint16_t> img((size_t)k * 4 * BQ + (tv ? (size_t)k * 32 : 0), 0);
     if (tv) {
-        uint16_t *kt = img.data() + (size_t)k * 4 * BG * 64;
+        uint16_t *kt = img.data() + (size_t)k * 4 * BQ;
         for (uint32_t r = 0; r < k; r++)
             for (uint32_t b = 0; b < 16; b++)
                 kt[((size_t)r * 16 + b) * 2] = kt[((size_t)r * 16 + b) * 2 + 1] =
@@ -235,12 +240,12 @@ inline std::vector<uint16_t> mat_image(uint32_t k, uint32_t rows, const uint16_t
     }
     for (uint32_t r = 0; r < k; r++)
         for (uint32_t q = 0; q < 4; q++) {
-            uint16_t *blk = img.data() + ((size_t)r * 4 + q) * BG * 64;
+            uint16_t *blk = img.data() + ((size_t)r * 4 + q) * BQ;
             for (uint32_t row = 0; row < (tv ? rows - 1 : rows); row++) {
                 const uint32_t g = row / 4, j = row % 4;
                 const uint16_t c = M[(size_t)row * k + r];
                 for (uint32_t n = 0; n < 16; n++) {
-                    const size_t at = g < 2 * NP ? (g / 2) * 128 + n * 8 + (g % 2) * 4 + j : NP * 128 + n * 4 + j;
+                    const size_t at = g < 2 * NP ? (g / 2) * 128 + n * 8 + (g % 2) * 4 + j : NP * 128 + n * TBu + j;
                     blk[at] = T.gmul((uint16_t)(n << (4 * q)), c);
                 }
             }

@@ -1,6 +1,6 @@
 // Host check of rs16::mat_image (tape_amd/csrc/rs16.hpp), the lookup image rs16_matrix_kernel
 // (rs16.hip) stages: the kernel's reads are emulated here -- per input and nibble position q the
-// 8-row pair entries at h * 128 + n * 8 (+ the 4-row tail group at NP * 128 + n * 4 for odd G), or
+// 8-row pair entries at h * 128 + n * 8 (+ the tail group at NP * 128 + n * 1 / 2 / 4 for odd G), or
 // with the VALU tail (tv, rows = 8 h + 1) the pairs only and the per-input bit constants K[b]
 // XORed over the set bits of the element -- and compared with the direct product sum_r M[i][r] *
 // x[r] over GF(2^16), for random and encode matrices (rs16::encode_matrix against
@@ -15,17 +15,21 @@
 
 using namespace tec::rs16;
 
-static int check(uint32_t k, uint32_t rows, const std::vector<uint16_t> &M, bool tv_req, std::mt19937_64 &rng) {
+// tail_bytes: the odd last group's entry size (2 / 4 / 8 B); narrow entries must still hold every
+// row of that group, so 2 B serves one row and 4 B two
+static int check(uint32_t k, uint32_t rows, const std::vector<uint16_t> &M, bool tv_req, uint32_t tail_bytes,
+                 std::mt19937_64 &rng) {
     const Tables &T = tables();
     const bool tv = tv_req && rows % 8 == 1 && rows > 1;
-    const std::vector<uint16_t> img = mat_image(k, rows, M.data(), tv_req);
-    const uint32_t G = (rows + 3) / 4, NP = G / 2, BG = tv ? 2 * NP : G;
-    const size_t want_size = (size_t)k * 4 * BG * 64 + (tv ? (size_t)k * 32 : 0);
+    const std::vector<uint16_t> img = mat_image(k, rows, M.data(), tv_req, tail_bytes);
+    const uint32_t G = (rows + 3) / 4, NP = G / 2;
+    const uint32_t TBu = (G % 2 && !tv) ? tail_bytes / 2 : 0, BQ = NP * 128 + 16 * TBu;
+    const size_t want_size = (size_t)k * 4 * BQ + (tv ? (size_t)k * 32 : 0);
     if (img.size() != want_size) {
         printf("size k=%u rows=%u tv=%d: %zu != %zu\n", k, rows, tv, img.size(), want_size);
         return 1;
     }
-    const uint16_t *kt = img.data() + (size_t)k * 4 * BG * 64;
+    const uint16_t *kt = img.data() + (size_t)k * 4 * BQ;
     int bad = 0;
     for (int col = 0; col < 64; col++) {
         std::vector<uint16_t> x(k);
@@ -33,12 +37,12 @@ static int check(uint32_t k, uint32_t rows, const std::vector<uint16_t> &M, bool
         std::vector<uint16_t> got(4 * G, 0);
         for (uint32_t r = 0; r < k; r++)
             for (uint32_t q = 0; q < 4; q++) {
-                const uint16_t *blk = img.data() + ((size_t)r * 4 + q) * BG * 64;
+                const uint16_t *blk = img.data() + ((size_t)r * 4 + q) * BQ;
                 const uint32_t n = (x[r] >> (4 * q)) & 15;
                 for (uint32_t h = 0; h < NP; h++)
                     for (uint32_t j = 0; j < 8; j++) got[8 * h + j] ^= blk[h * 128 + n * 8 + j];
                 if (G % 2 && !tv)
-                    for (uint32_t j = 0; j < 4; j++) got[8 * NP + j] ^= blk[NP * 128 + n * 4 + j];
+                    for (uint32_t j = 0; j < TBu; j++) got[8 * NP + j] ^= blk[NP * 128 + n * TBu + j];
             }
         if (tv)
             for (uint32_t r = 0; r < k; r++)
@@ -70,7 +74,10 @@ int main() {
             if ((size_t)k * ((rows + 3) / 4) * 512 > 80 * 1024) continue;
             std::vector<uint16_t> M((size_t)rows * k);
             for (auto &v : M) v = (uint16_t)rng();
-            for (int tv = 0; tv < 2; tv++, cases++) bad += check(k, rows, M, tv, rng);
+            const uint32_t G = (rows + 3) / 4, t = rows - 8 * (G / 2);
+            const uint32_t narrow = (G % 2 && t <= 2) ? 2 * t : 8;  // kernels.hpp rs16_mat_tail_bytes
+            for (int tv = 0; tv < 2; tv++, cases++) bad += check(k, rows, M, tv, 8, rng);
+            if (narrow != 8) cases++, bad += check(k, rows, M, false, narrow, rng);
         }
     // encode matrices: column r of E = the encode of unit vector e_r
     const uint32_t shapes[][2] = {{17, 33}, {16, 48}, {20, 40}, {5, 69}, {31, 40}, {17, 9}, {3, 17}};
@@ -90,7 +97,11 @@ int main() {
             }
         }
         if ((size_t)k * ((m + 3) / 4) * 512 <= 80 * 1024)
-            for (int tv = 0; tv < 2; tv++, cases++) bad += check(k, m, E, tv, rng);
+            for (int tv = 0; tv < 2; tv++, cases++) bad += check(k, m, E, tv, 8, rng);
+        {
+            const uint32_t G = (m + 3) / 4, t = m - 8 * (G / 2);
+            if (G % 2 && t <= 2 && (size_t)k * ((m + 3) / 4) * 512 <= 80 * 1024) cases++, bad += check(k, m, E, false, 2 * t, rng);
+        }
     }
     printf("%d cases, %d mismatches\n", cases, bad);
     return bad ? 1 : 0;
