@@ -77,11 +77,78 @@ def dist_setup(torch, dist, backend: str):
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            init_rccl(torch, dist, rank, local, world)
         else:
             dist.init_process_group(backend)
     return world, rank, local
+
+
+RCCL_INIT_TIMEOUT_S = 180
+
+
+def init_rccl(torch, dist, rank: int, local: int, world: int, timeout_s: float = RCCL_INIT_TIMEOUT_S) -> None:
+    """The one place a bench rank brings up RCCL (torch's "nccl" backend on ROCm).  It binds the rank
+    to cuda:LOCAL_RANK, creates the process group with a bounded timeout and runs one all_reduce so
+    the communicator is built here rather than inside the timed region.  Any failure -- no such
+    device, a rendezvous or communicator error, a wrong sum -- prints the rank, its device and the
+    error to stderr and exits non-zero, so a first multi-GPU run fails loudly (launch_ranks then
+    stops the other ranks) instead of hanging.  This branch has only ever run on the driver's
+    8-GPU node; the gloo branch is what the CPU tests exercise."""
+    import datetime
+    where = f"rank {rank}/{world} on cuda:{local}"
+    try:
+        ndev = torch.cuda.device_count()
+        if local >= ndev:
+            raise RuntimeError(f"LOCAL_RANK {local} but only {ndev} visible device(s)")
+        torch.cuda.set_device(local)
+        try:
+            p = torch.cuda.get_device_properties(local)
+            where += f" (pci {p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x})"
+        except Exception:
+            pass
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                timeout=datetime.timedelta(seconds=timeout_s))
+        t = torch.ones(1, dtype=torch.float64, device=torch.device("cuda", local))
+        dist.all_reduce(t)
+        torch.cuda.synchronize()
+        if int(t.item()) != world:
+            raise RuntimeError(f"first all_reduce summed to {t.item()}, expected {world}")
+    except BaseException as e:  # SystemExit / KeyboardInterrupt included: report, then leave non-zero
+        print(f"[bench] RCCL initialisation failed for {where}: {type(e).__name__}: {e}", file=sys.stderr,
+              flush=True)
+        os._exit(3)
+
+
+def step_rates(bytes_per_step: int, steps: int, elapsed_s: float, alg_bytes_per_launch: int | None = None,
+               kernel_ms_total: float | None = None, launches: int | None = None) -> dict:
+    """The arithmetic of every bench line, in one place (config 5 divided one
+    step's bytes by all steps' time).  `bytes_per_step` is the object bytes the whole job (all
+    ranks) encodes per step; `elapsed_s` covers `steps` steps (max over ranks).  Then
+        value [GiB/s] = bytes_per_step * steps / elapsed_s / 2^30,  ms_per_step = elapsed_s / steps * 1e3,
+    so value * ms_per_step * 2^30 / 1e3 == bytes_per_step exactly.  The roofline side: one launch
+    (one call's kernels) moves `alg_bytes_per_launch` algorithmic bytes; `kernel_ms_total` is the
+    device time of `launches` launches (HIP events on the launch stream)."""
+    if steps <= 0 or elapsed_s <= 0:
+        raise ValueError("steps and elapsed time must be positive")
+    out = {"value": bytes_per_step * steps / elapsed_s / 2**30, "ms_per_step": elapsed_s / steps * 1e3,
+           "avg_launch_ms": None, "achieved": None, "frac": None}
+    if kernel_ms_total is not None and launches:
+        avg_s = kernel_ms_total / launches / 1e3
+        out["avg_launch_ms"] = avg_s * 1e3
+        if alg_bytes_per_launch and avg_s > 0:
+            out["achieved"] = alg_bytes_per_launch / avg_s / 1e9
+            out["frac"] = out["achieved"] / PEAK_HBM_GBS
+    return out
+
+
+def config5_rates(total_objects: int, L: int, steps: int, rank_elapsed_s: list, kernel_ms_total: float,
+                  batches_per_step: int, device_batch: int) -> dict:
+    """Config 5's line values: one step = every rank encodes its whole share (all 16,384 objects
+    over the job) in `batches_per_step` device batches of `device_batch` objects."""
+    r = step_rates(total_objects * L, steps, max(rank_elapsed_s), ALG_BYTES["encode"] * device_batch
+                   if L == 4 * MiB else None, kernel_ms_total, steps * batches_per_step)
+    r["rank_ms_per_step"] = [x * 1e3 / steps for x in rank_elapsed_s]
+    return r
 
 
 # The kernels one step of each mode runs on the default workload (rocprofv3 names, prefix match).
@@ -254,6 +321,17 @@ def launcher_check(args) -> None:
     splitmix_fill(torch, buf, first, share, L)
     digests = [hashlib.sha256(buf[i * L:(i + 1) * L].numpy().tobytes()).hexdigest() for i in range(share)]
     t = max_over_ranks(torch, dist, world, 1.0 + rank, torch.device("cpu"))
+    # the line arithmetic on injected timings: rank r "took" (83.9 + r) ms per step, its kernels
+    # 10.43 ms per device batch -- the same functions the GPU run's line goes through
+    steps = args.steps
+    rank_el = gather_floats(torch, dist, world, steps * (0.0839 + 0.001 * rank), torch.device("cpu"))
+    if args.workload == "config5":
+        nbat = share // batch_objs
+        rates = config5_rates(share * world, L, steps, rank_el, steps * nbat * 10.43, nbat, batch_objs)
+        job_bytes = share * world * L
+    else:
+        rates = step_rates(share * world * L, steps, max(rank_el), None, steps * 10.43, steps)
+        job_bytes = share * world * L
     got = [None] * world
     if world > 1:
         dist.all_gather_object(got, {"rank": rank, "first": first, "end": end, "digests": digests,
@@ -265,7 +343,9 @@ def launcher_check(args) -> None:
                           "world_size": dist.get_world_size() if world > 1 else 1,
                           "backend": dist.get_backend() if world > 1 else None,
                           "objects_per_gpu": share, "device_batch_objects": batch_objs,
-                          "total_objects": share * world, "max_over_ranks_s": t, "ranks": got}), flush=True)
+                          "total_objects": share * world, "max_over_ranks_s": t, "ranks": got,
+                          "injected": {"steps": steps, "job_bytes_per_step": job_bytes, "rates": rates}}),
+              flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -500,16 +580,16 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    mine = time.perf_counter() - t0
     batch.kernel_timing(False)
     kms, kcalls = batch.kernel_time_ms()
-    elapsed = max_over_ranks(torch, dist, world, elapsed, dev)
+    ident = rank_identity(torch, dist, world, dev, mine, kms, args.steps)
+    elapsed = ident.pop("max_elapsed_s")
 
-    total_objs = nobj * world * args.steps
-    gib_s = total_objs * L / elapsed / 2**30
-    # device time of one step's kernels (recover = a decode and an encode enqueue per step)
-    avg_launch_s = kms / max(1, args.steps) / 1e3
-    achieved = (unit_bytes or 0) * nobj / avg_launch_s / 1e9 if unit_bytes else None
+    # one launch = one step's kernels (HIP events on the launch stream)
+    rates = step_rates(nobj * world * L, args.steps, elapsed, unit_bytes * nobj if unit_bytes else None,
+                       kms, args.steps)
+    achieved = rates["achieved"]
 
     verified = None  # the timed outputs, checked on the device against what they must equal
     if args.mode == "decode":
@@ -589,13 +669,13 @@ def main():
                 "device-resident slice-commitment GiB/s (hash_leaf x 20 + merkle root + proofs), batched 4 MiB "
                 "objects, 1 MI355X" if args.mode == "commit" else
                 f"device-resident {args.mode} GiB/s, batched 4 MiB objects, 1 MI355X"),
-            "value": round(gib_s, 3),
+            "value": round(rates["value"], 3),
             "unit": "GiB/s",
             "n_gpus": world,
             **comm_info(dist, world),
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(rates["ms_per_step"], 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -611,16 +691,17 @@ def main():
                        + f" of {nobj} x {L} B objects per GPU, Clay(20,7,16) rotated, 1 MB stripes",
                        "objects_per_gpu": nobj, "object_bytes": L, "profile": "clay(20,7,16)",
                        "parallelism": f"objects partitioned over {world} GPU(s)"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4) if achieved else None,
+            "roofline": {"bound": "hbm", "achieved": rnd(achieved, 1), "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": rnd(rates["frac"], 4),
                          "traffic": traffic,
                          "alg_bytes_per_launch": unit_bytes * nobj if unit_bytes else None,
-                         "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                         "avg_launch_ms": rnd(rates["avg_launch_ms"], 4),
                          "box_ceiling": ceiling,
                          "box_ceiling_frac": round(achieved / ceiling["blocks_GBps"], 4)
                          if ceiling and achieved else None},
             "cpu_baseline": cpu,
             "gpu": gpu_env(torch, dev),
+            "ranks": ident,
             "copy_inclusive": copy_inc,
             "copy_inclusive_encode_commit": copy_commit,
             "stream_sdk_shape": sdk_stream,
@@ -679,10 +760,10 @@ def config5_bench(args, torch, dist, world, rank, dev, np, T, batch):
     batch.kernel_timing(False)
     kms, _ = batch.kernel_time_ms()
     per_rank = gather_floats(torch, dist, world, mine, dev)
-    elapsed = max(per_rank)
+    rank_kms = gather_floats(torch, dist, world, kms / max(1, args.steps), dev)
+    rank_pci = gather_floats(torch, dist, world, float(pci_id(torch, dev)), dev)
     total = share * world
-    avg_launch_s = kms / max(1, args.steps * len(views)) / 1e3
-    achieved = ALG_BYTES["encode"] * nb / avg_launch_s / 1e9 if L == 4 * MiB else None
+    rates = config5_rates(total, L, args.steps, per_rank, kms, len(views), nb)
     # the timed outputs of the last batch: decode(slices 13..19) == the objects, on every rank
     metas = b"".join(d_out[i * per + g.slice_len - 48:i * per + g.slice_len].cpu().numpy().tobytes() for i in range(nb))
     dec_objs = batch.decode_descs([(i * per, g.slice_len, sum(1 << j for j in range(13, 20)), i * L) for i in range(nb)])
@@ -722,9 +803,9 @@ def config5_bench(args, torch, dist, world, rank, dev, np, T, batch):
         print(json.dumps({
             "metric": "device-resident encode GiB/s, 64 GiB stream of 4 MiB objects partitioned over the GPUs "
                       "(BASELINE config 5)",
-            "value": round(total * L / elapsed / 2**30, 3), "unit": "GiB/s", "n_gpus": world,
+            "value": round(rates["value"], 3), "unit": "GiB/s", "n_gpus": world,
             **comm_info(dist, world),
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(rates["ms_per_step"], 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (SplitMix64 per object, seed 0x7A9E5EED ^ id), device-resident",
             "config": {"workload": f"Slicer::encode of the 64 GiB stream ({total} x {L} B objects), {share} contiguous "
@@ -732,11 +813,13 @@ def config5_bench(args, torch, dist, world, rank, dev, np, T, batch):
                        "total_objects": total, "objects_per_gpu": share, "device_batch_objects": nb,
                        "object_bytes": L, "profile": "clay(20,7,16)",
                        "parallelism": f"objects partitioned over {world} GPU(s), no collective"},
-            "rank_ms_per_step": [round(x * 1e3 / args.steps, 3) for x in per_rank],
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4) if achieved else None,
+            "rank_ms_per_step": [round(x, 3) for x in rates["rank_ms_per_step"]],
+            "rank_kernel_ms_per_step": [round(x, 3) for x in rank_kms],
+            "rank_pci": [pci_str(int(x)) for x in rank_pci],
+            "roofline": {"bound": "hbm", "achieved": rnd(rates["achieved"], 1), "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": rnd(rates["frac"], 4),
                          "traffic": None, "alg_bytes_per_launch": ALG_BYTES["encode"] * nb,
-                         "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
+                         "avg_launch_ms": rnd(rates["avg_launch_ms"], 4)},
             "cpu_baseline": cpu, "gpu": gpu_env(torch, dev),
             "copy_inclusive": {"value": round(total * L / max(c_rank) / 2**30, 3), "unit": "GiB/s", "pinned": True,
                                "host_ring_objects": ring, "rank_ms": [round(x * 1e3, 1) for x in c_rank],
@@ -746,6 +829,34 @@ def config5_bench(args, torch, dist, world, rank, dev, np, T, batch):
             "outputs_verified": all(x == 1.0 for x in oks)}), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def rnd(x, nd):
+    return None if x is None else round(x, nd)
+
+
+def pci_id(torch, dev) -> int:
+    """The device's PCI address packed as domain << 16 | bus << 8 | device (0 when unknown)."""
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        return (p.pci_domain_id << 16) | (p.pci_bus_id << 8) | p.pci_device_id
+    except Exception:
+        return 0
+
+
+def pci_str(v: int) -> str:
+    return f"{v >> 16:04x}:{(v >> 8) & 0xFF:02x}:{v & 0xFF:02x}"
+
+
+def rank_identity(torch, dist, world: int, dev, elapsed_s: float, kernel_ms: float, steps: int) -> dict:
+    """Per-rank identity of a line: each rank's wall ms per step, its kernels' ms
+    per step and its device's PCI address, so an N > 1 line shows a slow or doubled-up rank."""
+    el = gather_floats(torch, dist, world, elapsed_s, dev)
+    return {"rank_ms_per_step": [round(x * 1e3 / steps, 4) for x in el],
+            "rank_kernel_ms_per_step": [round(x / max(1, steps), 4)
+                                        for x in gather_floats(torch, dist, world, kernel_ms, dev)],
+            "rank_pci": [pci_str(int(x)) for x in gather_floats(torch, dist, world, float(pci_id(torch, dev)), dev)],
+            "max_elapsed_s": max(el)}
 
 
 def gather_floats(torch, dist, world: int, x: float, dev) -> list:
@@ -803,7 +914,7 @@ def outer_bench(args, torch, dist, world, rank, dev):
     dec = outer.OuterCoder(k, n).decode([(k + j, seg0[j]) for j in range(k)])
     verified = dec == d_in[:k * cb].cpu().numpy().tobytes()
     alg = (k + m) * cb * segs
-    avg_s = kms / max(1, args.steps) / 1e3
+    er = step_rates(segs * world * k * cb, args.steps, elapsed, alg, kms, args.steps)
     # decode (snapshot reads, outer.rs:126-197) of every segment from its first 17 recovery
     # chunks (all data chunks missing: 17 restored per segment), device-resident
     d_dec = torch.empty(segs * k * cb, dtype=torch.uint8, device=dev)
@@ -828,13 +939,13 @@ def outer_bench(args, torch, dist, world, rank, dev):
     dkms, _ = batch.kernel_time_ms()
     dec_ok = bool(torch.equal(d_dec, d_in))
     dec_alg = 2 * k * cb * segs  # 17 received chunks read, 17 restored written, per segment
-    dec_s = dkms / max(1, args.steps) / 1e3
-    decode = {"value": round(segs * world * args.steps * k * cb / dec_elapsed / 2**30, 3), "unit": "GiB/s",
-              "ms_per_step": round(dec_elapsed / args.steps * 1e3, 4), "workload": "all 17 data chunks restored "
+    dr = step_rates(segs * world * k * cb, args.steps, dec_elapsed, dec_alg, dkms, args.steps)
+    decode = {"value": round(dr["value"], 3), "unit": "GiB/s",
+              "ms_per_step": round(dr["ms_per_step"], 4), "workload": "all 17 data chunks restored "
               "from 17 recovery chunks per segment (one te_outer_decode_device_batch call)",
-              "roofline": {"bound": "hbm", "achieved": round(dec_alg / dec_s / 1e9, 1), "peak": PEAK_HBM_GBS,
-                           "unit": "GB/s", "frac": round(dec_alg / dec_s / 1e9 / PEAK_HBM_GBS, 4),
-                           "alg_bytes_per_launch": dec_alg, "avg_launch_ms": round(dec_s * 1e3, 4)},
+              "roofline": {"bound": "hbm", "achieved": round(dr["achieved"], 1), "peak": PEAK_HBM_GBS,
+                           "unit": "GB/s", "frac": round(dr["frac"], 4),
+                           "alg_bytes_per_launch": dec_alg, "avg_launch_ms": round(dr["avg_launch_ms"], 4)},
               "outputs_verified": dec_ok}
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
@@ -854,16 +965,16 @@ def outer_bench(args, torch, dist, world, rank, dev):
     if rank == 0:
         print(json.dumps({
             "metric": "device-resident OuterCoder(17, 50) encode GiB/s of snapshot data, 4 MiB chunks, 1 MI355X",
-            "value": round(segs * world * args.steps * k * cb / elapsed / 2**30, 3), "unit": "GiB/s",
+            "value": round(er["value"], 3), "unit": "GiB/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(er["ms_per_step"], 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u16 (GF(2^16))", "data": "synthetic SplitMix64, device-resident",
             "config": {"workload": f"OuterCoder(17, 50).encode of {segs} segments of 17 x 4 MiB per GPU "
                                    "(reed-solomon-simd Leopard GF(2^16) construction, parity unpinned)",
                        "segments_per_gpu": segs, "chunk_bytes": cb, "parallelism": f"segments over {world} GPU(s)"},
-            "roofline": {"bound": "hbm", "achieved": round(alg / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(alg / avg_s / 1e9 / PEAK_HBM_GBS, 4), "traffic": traffic["outer"],
-                         "alg_bytes_per_launch": alg, "avg_launch_ms": round(avg_s * 1e3, 4)},
+            "roofline": {"bound": "hbm", "achieved": round(er["achieved"], 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(er["frac"], 4), "traffic": traffic["outer"],
+                         "alg_bytes_per_launch": alg, "avg_launch_ms": round(er["avg_launch_ms"], 4)},
             "cpu_baseline": cpu, "outputs_verified": verified, "decode": decode}), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -259,6 +259,10 @@ int te_encode_batch_host(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *h_
 int te_encode_batch_host_multi(te_clay *const *coders, size_t ncoders, const te_slicer_cfg *cfg,
                                const uint8_t *h_data, const te_object *objs, size_t nobj, uint8_t *h_out,
                                size_t window_bytes);
+/* Host only: the split te_encode_batch_host_multi uses.  cuts[0..nparts] (nparts + 1 entries):
+ * part p encodes objects [cuts[p], cuts[p+1]); contiguous, covering, by about equal input bytes
+ * (blob_len + 1 per object).  Parts may be empty when nobj < nparts. */
+int te_balance_object_ranges(const te_object *objs, size_t nobj, size_t nparts, size_t *cuts);
 /* te_encode_batch_host plus the slice commitments of BlobEncoder::encode_with_proofs
  * (sdk/src/codec/encoder.rs:220-260; the stream writer's per-chunk step, sdk/src/stream/write.rs:
  * 332-362): per object o, leaf hashes hash_leaf(slice i) at h_leaf_hashes + (o*n + i)*32, the

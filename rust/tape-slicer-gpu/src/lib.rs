@@ -99,6 +99,22 @@ pub(crate) fn repair_status(s: i32, missing: Option<SliceIndex>) -> Result<(), R
     }
 }
 
+/// ClayParams (lib/core/src/encoding.rs:180-239): n | k << 8 | d << 16 in one u64.  Restated so
+/// this file compiles on its own; inside lib/slicer `tape_core::encoding::ClayParams` replaces it.
+#[derive(Clone, Copy, Debug, PartialEq, Eq, Hash)]
+pub struct ClayParams { packed: u64 }
+impl ClayParams {
+    pub const DEFAULT: Self = Self::new(20, 7, 16);
+    pub const fn new(n: u8, k: u8, d: u8) -> Self { Self { packed: (n as u64) | ((k as u64) << 8) | ((d as u64) << 16) } }
+    pub const fn n(&self) -> u8 { (self.packed & 0xFF) as u8 }
+    pub const fn k(&self) -> u8 { ((self.packed >> 8) & 0xFF) as u8 }
+    pub const fn d(&self) -> u8 { ((self.packed >> 16) & 0xFF) as u8 }
+    pub const fn m(&self) -> u8 { self.n().saturating_sub(self.k()) }
+    pub const fn as_u64(&self) -> u64 { self.packed }
+    pub const fn from_u64(v: u64) -> Self { Self { packed: v } }
+}
+impl Default for ClayParams { fn default() -> Self { Self::DEFAULT } }
+
 /// ClayCoder (lib/slicer/src/clay.rs:13-122) with the GF(2^8) work on the GPU.  The reference's
 /// `pub clay: ClayCode` is never used outside its crate, so it has no counterpart.
 pub struct ClayCoder {
@@ -122,18 +138,21 @@ impl ClayCoder {
         Self { raw: NonNull::new(p).unwrap(), k, m: n - k, d, pool: PinnedPool::default() }
     }
 
-    /// clay.rs:37-39; `packed` is ClayParams' u64 (n | k << 8 | d << 16, encoding.rs:193-197).
-    pub fn from_params(packed: u64) -> Self {
-        let (n, k, d) = ((packed & 0xff) as usize, ((packed >> 8) & 0xff) as usize, ((packed >> 16) & 0xff) as usize);
-        assert!(n > k && k > 0 && d >= k + 1 && d <= n - 1, "invalid ClayParams");
+    /// clay.rs:37-39: `Self::new(params.n(), params.k(), params.d())`, with new()'s asserts.
+    pub fn from_params(params: ClayParams) -> Self {
+        let (n, k, d) = (params.n() as usize, params.k() as usize, params.d() as usize);
+        assert!(n > k, "n must be > k");
+        assert!(k > 0, "k must be > 0");
+        assert!(d >= k + 1, "d must be >= k + 1");
+        assert!(d <= n - 1, "d must be <= n - 1");
         let mut p = std::ptr::null_mut();
-        let r = unsafe { ffi::te_clay_from_params(packed, &mut p) };
+        let r = unsafe { ffi::te_clay_from_params(params.as_u64(), &mut p) };
         if r != 0 { fatal(r) }
         Self { raw: NonNull::new(p).unwrap(), k, m: n - k, d, pool: PinnedPool::default() }
     }
 
-    /// The packed ClayParams of this coder (what the Slicer's profile carries).
-    pub fn params(&self) -> u64 { (self.n() as u64) | (self.k as u64) << 8 | (self.d as u64) << 16 }
+    /// The ClayParams of this coder (what the Slicer's profile carries).
+    pub fn params(&self) -> ClayParams { ClayParams::new(self.n() as u8, self.k as u8, self.d as u8) }
 
     fn info(&self) -> ffi::te_clay_info {
         let mut i = ffi::te_clay_info { n: 0, k: 0, m: 0, d: 0, q: 0, t: 0, nu: 0, alpha: 0, beta: 0 };
@@ -321,12 +340,19 @@ impl Drop for PinnedBuf {
 }
 
 /// Pinned buffers reused across windows (hipHostMalloc is far too slow to call per window).
+/// Holds at most `PinnedPool::KEEP` free buffers (it kept every larger buffer it had
+/// ever allocated for the coder's lifetime); take() hands out the smallest one that fits.
 #[derive(Default)]
 pub struct PinnedPool { free: Vec<PinnedBuf> }
 impl PinnedPool {
-    /// A buffer of at least `len` bytes, visible length `len`.
+    pub const KEEP: usize = 2;
+    /// A buffer of at least `len` bytes, visible length `len`.  Its bytes are NOT cleared on reuse:
+    /// every caller in this crate hands it to a library call that writes all `len` bytes (the
+    /// packed input is copied in whole; te_encode_commit_batch_host writes every slice byte).
     pub fn take(&mut self, len: usize) -> PinnedBuf {
-        let mut b = match self.free.iter().position(|b| b.capacity() >= len) {
+        let best = self.free.iter().enumerate().filter(|(_, b)| b.capacity() >= len).min_by_key(|(_, b)| b.capacity())
+            .map(|(i, _)| i);
+        let mut b = match best {
             Some(i) => self.free.swap_remove(i),
             None => PinnedBuf::new(len),
         };
@@ -334,7 +360,14 @@ impl PinnedPool {
         b.set_len(len);
         b
     }
-    pub fn give(&mut self, b: PinnedBuf) { self.free.push(b) }
+    /// Return a buffer; beyond KEEP free buffers the smallest is released (freed now).
+    pub fn give(&mut self, b: PinnedBuf) {
+        self.free.push(b);
+        while self.free.len() > Self::KEEP {
+            let i = (0..self.free.len()).min_by_key(|&i| self.free[i].capacity()).unwrap();
+            drop(self.free.swap_remove(i));
+        }
+    }
 }
 
 /// One window of the stream writer (sdk/src/stream/write.rs:332-362): every object's n slices
@@ -344,7 +377,7 @@ pub struct EncodedWindow { pub slices: PinnedBuf, pub leaf_hashes: Vec<u8>, pub 
 /// The Slicer configuration of a coder's objects: rotated layout, this coder's ClayParams in the
 /// metadata suffix (not the default profile unless the coder is Clay(20,7,16)).
 pub(crate) fn slicer_cfg(coder: &ClayCoder, rotated: bool, chunk_index: u64) -> ffi::te_slicer_cfg {
-    ffi::te_slicer_cfg { rotated: rotated as i32, encoding: ffi::TE_ENCODING_CLAY, params: coder.params(), chunk_index }
+    ffi::te_slicer_cfg { rotated: rotated as i32, encoding: ffi::TE_ENCODING_CLAY, params: coder.params().as_u64(), chunk_index }
 }
 
 /// Objects laid out back to back in one pinned buffer from `pool` (one descriptor each; the only

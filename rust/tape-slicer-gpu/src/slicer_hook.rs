@@ -72,11 +72,52 @@ impl ObjectCoder for ClayCoder {
     }
 }
 
-/// RepairPlan (repair.rs:16-47) as the library holds it.
-pub struct RepairPlan { raw: *mut ffi::te_repair_plan }
+/// RepairPlan (repair.rs:16-28) with the reference's public fields, read back from the library's
+/// plan when it is built, so callers that walk `plan.stripes` (the node's per_helper_reqs,
+/// network/node/src/features/spool/repair.rs:468-491) read it unchanged; the library handle it was
+/// read from is kept for extract / repair.
+pub struct RepairPlan {
+    /// The slice being repaired.
+    pub lost: SliceIndex,
+    /// Number of stripes in the blob.
+    pub num_stripes: u32,
+    /// Full chunk size per stripe (bytes).
+    pub chunk_size: u64,
+    /// Sub-chunk size (chunk_size / alpha).
+    pub sub_chunk_size: u64,
+    /// Per-stripe repair plans.
+    pub stripes: Vec<StripeRepair>,
+    raw: *mut ffi::te_repair_plan,
+}
+/// StripeRepair (repair.rs:30-38).
+pub struct StripeRepair { pub stripe: u32, pub lost_shard: SliceIndex, pub helpers: Vec<HelperPlan> }
+/// HelperPlan (repair.rs:40-47).
+pub struct HelperPlan { pub slice: SliceIndex, pub shard: SliceIndex, pub sub_chunks: Vec<u32> }
 impl Drop for RepairPlan { fn drop(&mut self) { unsafe { ffi::te_repair_plan_free(self.raw) } } }
+unsafe impl Send for RepairPlan {}
 
 impl RepairPlan {
+    /// The pub fields from the library's plan (te_repair_plan_get_info + te_repair_plan_stripe).
+    fn wrap(raw: *mut ffi::te_repair_plan) -> Self {
+        let mut info = ffi::te_repair_plan_info { lost: 0, num_stripes: 0, d: 0, beta: 0, chunk_size: 0, sub_chunk_size: 0 };
+        unsafe { ffi::te_repair_plan_get_info(raw, &mut info) };
+        let (d, beta) = (info.d as usize, info.beta as usize);
+        let mut stripes = Vec::with_capacity(info.num_stripes as usize);
+        for s in 0..info.num_stripes {
+            let (mut lost_shard, mut slices, mut shards, mut subs) = (0u32, vec![0u32; d], vec![0u32; d], vec![0u32; d * beta]);
+            unsafe {
+                ffi::te_repair_plan_stripe(raw, s, &mut lost_shard, slices.as_mut_ptr(), shards.as_mut_ptr(), subs.as_mut_ptr())
+            };
+            let helpers = (0..d)
+                .map(|h| HelperPlan { slice: SliceIndex::new(slices[h] as usize), shard: SliceIndex::new(shards[h] as usize),
+                                      sub_chunks: subs[h * beta..(h + 1) * beta].to_vec() })
+                .collect();
+            stripes.push(StripeRepair { stripe: s, lost_shard: SliceIndex::new(lost_shard as usize), helpers });
+        }
+        Self { lost: SliceIndex::new(info.lost as usize), num_stripes: info.num_stripes, chunk_size: info.chunk_size,
+               sub_chunk_size: info.sub_chunk_size, stripes, raw }
+    }
+
     /// Slicer::repair_plan_from_params (repair.rs:137-201): blob_len / stripe_size from TrackInfo.
     pub fn from_params(coder: &ClayCoder, rotated: bool, lost: SliceIndex, available: &[SliceIndex], blob_len: u64,
                        stripe_size: u64) -> Result<Self, RepairError> {
@@ -87,7 +128,7 @@ impl RepairPlan {
                                             blob_len, stripe_size, &mut p)
         };
         repair_status(r, None)?;
-        Ok(Self { raw: p })
+        Ok(Self::wrap(p))
     }
     /// Slicer::repair_plan (repair.rs:203-281): geometry from a reference slice's suffix.
     pub fn from_slice(coder: &ClayCoder, rotated: bool, lost: SliceIndex, available: &[SliceIndex], reference: &[u8])
@@ -99,7 +140,7 @@ impl RepairPlan {
                                            reference.as_ptr(), reference.len(), &mut p)
         };
         repair_status(r, None)?;
-        Ok(Self { raw: p })
+        Ok(Self::wrap(p))
     }
 
     /// extract_repair_data (repair.rs:97-130): the helper-side gather of its planned sub-chunks.
@@ -127,9 +168,7 @@ impl RepairPlan {
             ptrs[**i] = d.as_ptr();
             lens[**i] = d.len();
         }
-        let mut info = ffi::te_repair_plan_info { lost: 0, num_stripes: 0, d: 0, beta: 0, chunk_size: 0, sub_chunk_size: 0 };
-        unsafe { ffi::te_repair_plan_get_info(self.raw, &mut info) };
-        let mut out = vec![0u8; info.num_stripes as usize * info.chunk_size as usize + ffi::TE_META_SIZE as usize];
+        let mut out = vec![0u8; self.num_stripes as usize * self.chunk_size as usize + ffi::TE_META_SIZE as usize];
         let r = unsafe {
             ffi::te_slicer_repair(coder.raw.as_ptr(), self.raw, ptrs.as_ptr(), lens.as_ptr(), metadata.as_ptr(),
                                   out.as_mut_ptr(), out.len())

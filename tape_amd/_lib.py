@@ -145,6 +145,7 @@ def _load() -> C.CDLL:
         "te_serve_repair_request": (i, [vp, u8p, sz, u32p, u32p, u32p, sz, u8p, sz, szp]),
         "te_encode_batch_device": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz, vp, vp]),
         "te_encode_batch_host": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz, vp, sz]),
+        "te_balance_object_ranges": (i, [C.POINTER(te_object), sz, sz, C.POINTER(sz)]),
         "te_encode_batch_host_multi": (i, [C.POINTER(vp), sz, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz,
                                            vp, sz]),
         "te_encode_commit_batch_host": (i, [vp, C.POINTER(te_slicer_cfg), vp, C.POINTER(te_object), sz, vp,

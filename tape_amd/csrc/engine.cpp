@@ -28,6 +28,7 @@
 #include "clay_host.hpp"
 #include "rs16.hpp"
 #include "host_hash.hpp"
+#include "copy_pool.hpp"
 
 using namespace tec;
 
@@ -203,84 +204,16 @@ struct ReaderEvents {
     }
 };
 
-// Host memcpy fan-out for the per-call entry points: a few persistent threads (plus the caller)
-// copy a list of segments, big segments split into 64 KiB pieces.  Used to gather a call's
-// scattered host buffers (Slicer::repair's d helper buffers, repair.rs:340-354) into one pinned
-// staging buffer -- one H2D instead of one driver-staged copy per helper -- and to scatter the
-// result back into the caller's (pageable) buffer.
-class CopyPool {
-  public:
-    struct Seg {
-        void *dst;
-        const void *src;
-        size_t len;
-    };
-    static CopyPool &get() {
-        static CopyPool *p = new CopyPool();  // never destroyed (workers outlive static destructors)
-        return *p;
-    }
-    void run(const std::vector<Seg> &segs) {
-        constexpr size_t kPiece = 64 << 10;
-        std::lock_guard<std::mutex> one(call_mu_);  // one job at a time
-        pieces_.clear();
-        size_t total = 0;
-        for (const Seg &g : segs)
-            for (size_t o = 0; o < g.len; o += kPiece) {
-                const size_t l = std::min(kPiece, g.len - o);
-                pieces_.push_back({static_cast<uint8_t *>(g.dst) + o, static_cast<const uint8_t *>(g.src) + o, l});
-                total += l;
-            }
-        if (pieces_.size() <= 1 || total < (128u << 10) || workers_.empty()) {  // not worth waking anyone
-            for (const Seg &g : pieces_) memcpy(g.dst, g.src, g.len);
-            return;
-        }
-        next_.store(0);
-        done_.store(0);
-        {
-            std::lock_guard<std::mutex> g(m_);
-            gen_++;
-        }
-        cv_.notify_all();
-        work();
-        std::unique_lock<std::mutex> g(m_);
-        cv_done_.wait(g, [&] { return done_.load() == pieces_.size(); });
-    }
-
-  private:
-    CopyPool() {
-        const int n = std::max(0, std::min(3, hh::default_threads() - 1));
-        for (int i = 0; i < n; i++)
-            workers_.emplace_back([this] {
-                uint64_t seen = 0;
-                for (;;) {
-                    {
-                        std::unique_lock<std::mutex> g(m_);
-                        cv_.wait(g, [&] { return gen_ != seen; });
-                        seen = gen_;
-                    }
-                    work();
-                }
-            });
-        for (auto &t : workers_) t.detach();
-    }
-    void work() {
-        for (;;) {
-            const size_t i = next_.fetch_add(1);
-            if (i >= pieces_.size()) return;
-            memcpy(pieces_[i].dst, pieces_[i].src, pieces_[i].len);
-            if (done_.fetch_add(1) + 1 == pieces_.size()) {
-                std::lock_guard<std::mutex> g(m_);
-                cv_done_.notify_all();
-            }
-        }
-    }
-    std::mutex call_mu_, m_;
-    std::condition_variable cv_, cv_done_;
-    std::vector<Seg> pieces_;
-    std::atomic<size_t> next_{0}, done_{0};
-    uint64_t gen_ = 0;
-    std::vector<std::thread> workers_;
-};
+// One copy pool per device, so per-call copies of handles on different GPUs do not queue behind
+// one another.  Three workers plus the calling thread.
+static tec::CopyPool &copy_pool(int device) {
+    static std::mutex mu;
+    static tec::CopyPool *pools[65] = {};
+    const int slot = device < 0 || device >= 64 ? 64 : device;
+    std::lock_guard<std::mutex> g(mu);
+    if (!pools[slot]) pools[slot] = new tec::CopyPool(std::max(0, std::min(3, hh::default_threads() - 1)));
+    return *pools[slot];
+}
 
 struct DevBuf {
     void *p = nullptr;
@@ -3018,23 +2951,31 @@ void te_stream_writer_free(te_stream_writer *w) {
     delete w;
 }
 
+int te_balance_object_ranges(const te_object *objs, size_t nobj, size_t nparts, size_t *cuts) {
+    if (!cuts || nparts == 0 || (!objs && nobj)) return TE_ERR_INVALID_ARG;
+    // contiguous ranges of about equal input bytes (+1 per object, so empty blobs count too):
+    // cut p is the first object index after which the running byte count reaches p/nparts of the total
+    uint64_t total = 0;
+    for (size_t i = 0; i < nobj; i++) total += objs[i].blob_len + 1;
+    for (size_t p = 0; p <= nparts; p++) cuts[p] = nobj;
+    cuts[0] = 0;
+    unsigned __int128 acc = 0;
+    size_t part = 1;
+    for (size_t i = 0; i < nobj && part < nparts; i++) {
+        acc += objs[i].blob_len + 1;
+        while (part < nparts && acc * nparts >= (unsigned __int128)total * part) cuts[part++] = i + 1;
+    }
+    return TE_OK;
+}
+
 int te_encode_batch_host_multi(te_clay *const *coders, size_t ncoders, const te_slicer_cfg *cfg, const uint8_t *h_data,
                                const te_object *objs, size_t nobj, uint8_t *h_out, size_t window_bytes) {
     if (!coders || ncoders == 0 || !cfg || (!objs && nobj)) return TE_ERR_INVALID_ARG;
     for (size_t i = 0; i < ncoders; i++)
         if (!coders[i]) return TE_ERR_INVALID_ARG;
     if (ncoders == 1 || nobj <= 1) return te_encode_batch_host(coders[0], cfg, h_data, objs, nobj, h_out, window_bytes);
-    // contiguous ranges of about equal input bytes
-    uint64_t total = 0;
-    for (size_t i = 0; i < nobj; i++) total += objs[i].blob_len + 1;
-    std::vector<size_t> cut(ncoders + 1, nobj);
-    cut[0] = 0;
-    uint64_t acc = 0;
-    size_t part = 1;
-    for (size_t i = 0; i < nobj && part < ncoders; i++) {
-        acc += objs[i].blob_len + 1;
-        while (part < ncoders && acc * ncoders >= total * part) cut[part++] = i + 1;
-    }
+    std::vector<size_t> cut(ncoders + 1);
+    (void)te_balance_object_ranges(objs, nobj, ncoders, cut.data());
     std::vector<int> rc(ncoders, TE_OK);
     std::vector<std::string> why(ncoders);  // each worker's te_last_error_detail (thread-local)
     std::vector<std::thread> th;
@@ -3366,33 +3307,36 @@ int te_clay_encode(te_clay *c, const uint8_t *data, size_t len, uint8_t *chunks,
 
 }  // extern "C"
 // The given slices (n pointers, null = absent) to c->io_in at i * len, on c->stream.  Page-locked
-// ones are copied directly; short pageable ones are first gathered into the handle's pinned
-// staging by the copy pool: each pageable H2D goes through the driver's staging at ~57 us of
-// fixed cost (te_slicer_decode, 7 x 715 KB: 1.11 -> 0.81 ms per 4 MiB call, against 0.70 with
-// pinned slices, r05).  Long ones go to the driver, whose pageable path outruns the 4-thread
-// memcpy there (7 x 11.4 MB, 64 MiB object: 3.03 ms direct, 4.2-4.5 gathered).
+// ones, and long ones, are copied directly; only the short pageable ones are first gathered into
+// the handle's pinned staging by the device's copy pool (one pageable slice used to
+// send every slice, pinned ones included, through the gather): each pageable H2D goes through the
+// driver's staging at ~57 us of fixed cost (te_slicer_decode, 7 x 715 KB: 1.11 -> 0.81 ms per
+// 4 MiB call, against 0.70 with pinned slices, r05).  Long ones go to the driver, whose pageable
+// path outruns the 4-thread memcpy there (7 x 11.4 MB, 64 MiB object: 3.03 ms direct, 4.2-4.5
+// gathered).
 constexpr size_t kGatherMaxSlice = 2u << 20;
 static int upload_slices(te_clay *c, const uint8_t *const *slices, size_t len) {
     const int n = c->h.n;
-    bool direct = true;  // every slice page-locked, or long
-    int given = 0;
-    for (int i = 0; i < n; i++)
-        if (slices[i]) given++, direct = direct && (len > kGatherMaxSlice || host_pinned(slices[i]));
     const uint8_t *src[64];
-    if (!direct) {
-        TE_HIP(c->hio_in.ensure((size_t)given * len));
-        std::vector<CopyPool::Seg> segs;
+    int gather = 0;
+    for (int i = 0; i < n; i++) {
+        src[i] = slices[i];
+        if (slices[i] && len <= kGatherMaxSlice && !host_pinned(slices[i])) gather++;
+    }
+    if (gather) {
+        TE_HIP(c->hio_in.ensure((size_t)gather * len));
+        std::vector<tec::CopyPool::Seg> segs;
         for (int i = 0, g = 0; i < n; i++)
-            if (slices[i]) {
+            if (slices[i] && len <= kGatherMaxSlice && !host_pinned(slices[i])) {
                 src[i] = c->hio_in.u8() + (size_t)g++ * len;
                 segs.push_back({const_cast<uint8_t *>(src[i]), slices[i], len});
             }
-        CopyPool::get().run(segs);
+        copy_pool(c->device).run(segs);
     }
     for (int i = 0; i < n; i++)
         if (slices[i])
-            TE_HIP(hipMemcpyAsync(c->io_in.as<uint8_t>() + (size_t)i * len, direct ? slices[i] : src[i], len,
-                                  hipMemcpyHostToDevice, c->stream));
+            TE_HIP(hipMemcpyAsync(c->io_in.as<uint8_t>() + (size_t)i * len, src[i], len, hipMemcpyHostToDevice,
+                                  c->stream));
     return TE_OK;
 }
 extern "C" {
@@ -3641,10 +3585,10 @@ int te_slicer_repair(te_clay *c, const te_repair_plan *p, const uint8_t *const *
     // repaired slice back through staging: per call two DMA copies, not d + 1 driver-staged ones
     TE_HIP(c->hio_in.ensure(total + 16));
     TE_HIP(c->hio_out.ensure(out_bytes));
-    std::vector<CopyPool::Seg> segs;
+    std::vector<tec::CopyPool::Seg> segs;
     for (uint32_t sl = 0; sl < p->n; sl++)
         if (need[sl]) segs.push_back({c->hio_in.u8() + off[sl], helper_data[sl], need[sl]});
-    CopyPool::get().run(segs);
+    copy_pool(c->device).run(segs);
     // the kernels read the helpers from and write the slice to the pinned staging directly, over
     // PCIe, with no H2D / D2H copy: 0.131 -> 0.103 ms per 4 MiB call, 0.85 -> 0.73 ms at 64 MiB
     // (r05, scripts/gpu_percall_zc.sh; the repair kernels only read their inputs and write their
@@ -3663,7 +3607,7 @@ int te_slicer_repair(te_clay *c, const te_repair_plan *p, const uint8_t *const *
     TE_HIP(hipStreamSynchronize(c->stream));  // (an event spin-wait measured no better: 0.146 vs 0.132-0.139 ms, r05)
     // (pipelining the gather with the H2D in four pieces and the scatter with the D2H in two
     // halves measured slower: 0.17 against 0.134-0.143 ms per 4 MiB call, r05)
-    CopyPool::get().run({{out, c->hio_out.p, out_bytes}});
+    copy_pool(c->device).run({{out, c->hio_out.p, out_bytes}});
     return TE_OK;
 }
 

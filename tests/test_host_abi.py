@@ -281,3 +281,50 @@ def test_outer_decode_batch_argument_checks():
     if _lib.device_count() == 0:
         assert call([full, two_missing, two_missing]) == _lib.TE_ERR_NO_DEVICE
         assert call([full], seg_out=0) == _lib.TE_ERR_NO_DEVICE  # one segment: seg_out unused
+
+
+def _ranges(lens, nparts):
+    objs = (_lib.te_object * max(1, len(lens)))()
+    for i, l in enumerate(lens):
+        objs[i].blob_len = l
+    cuts = (C.c_size_t * (nparts + 1))()
+    assert _lib.lib.te_balance_object_ranges(objs, len(lens), nparts, cuts) == 0
+    return list(cuts)
+
+
+def test_balance_object_ranges():
+    """te_encode_batch_host_multi's split (pure host code): contiguous ranges that
+    cover every object once, in order, each part's bytes within one object of total / nparts."""
+    rnd = random.Random(7)
+    for trial in range(200):
+        nobj = rnd.choice([0, 1, 2, 3, 7, 64, 1000])
+        nparts = rnd.choice([1, 2, 3, 4, 8])
+        lens = [rnd.choice([0, 1, 4 << 20, rnd.randrange(1, 8 << 20)]) for _ in range(nobj)]
+        cuts = _ranges(lens, nparts)
+        assert cuts[0] == 0 and cuts[-1] == nobj and cuts == sorted(cuts)
+        w = [l + 1 for l in lens]
+        total, biggest = sum(w), max(w, default=0)
+        for p in range(nparts):
+            part = sum(w[cuts[p]:cuts[p + 1]])
+            assert abs(part - total / nparts) <= biggest, (trial, p, part, total / nparts)
+    assert _ranges([4 << 20] * 8, 8) == list(range(9))      # equal objects: one each
+    assert _ranges([4 << 20] * 16, 4) == [0, 4, 8, 12, 16]
+    assert _ranges([100], 4)[-1] == 1
+
+
+def test_encode_batch_host_multi_joins_without_device():
+    """The per-handle threads of te_encode_batch_host_multi start, fail (no device) and are all
+    joined; the first handle's status comes back on the calling thread, with its detail text."""
+    if T.device_count() > 0:
+        pytest.skip("device present")
+    from tape_amd import batch
+    slicers = [T.Slicer.clay_default() for _ in range(4)]
+    L = 1000
+    buf_in = bytearray(8 * L)
+    buf_out = bytearray(8 * 20 * 4000)
+    import numpy as np
+    a_in = np.frombuffer(buf_in, np.uint8)
+    a_out = np.frombuffer(buf_out, np.uint8)
+    for _ in range(20):  # repeated: every thread is joined each time (no leak, no hang)
+        with pytest.raises(T.NoDeviceError):
+            batch.encode_batch_host_multi(slicers, a_in, [(i * L, L, i * 20 * 4000, 0) for i in range(8)], a_out)

@@ -66,3 +66,24 @@ def test_shim_mirrors_reference_items():
               "Clay(String)", "MissingHelper(SliceIndex)"):
         assert v in src, v
     assert "TE_CLAY_DEFAULT_PARAMS" not in src.split("fn encode_with_proofs_batch")[1]
+
+
+def test_shim_reference_signatures():
+    """ClayCoder::from_params takes ClayParams (clay.rs:37-39, called that way at
+    network/node/src/features/spool/repair.rs:313,506), and RepairPlan exposes the reference's pub
+    fields (repair.rs:16-47; the node walks plan.stripes, repair.rs:476)."""
+    src_dir = os.path.join(ROOT, "rust", "tape-slicer-gpu", "src")
+    lib_rs = open(os.path.join(src_dir, "lib.rs")).read()
+    hook = open(os.path.join(src_dir, "slicer_hook.rs")).read()
+    assert "pub fn from_params(params: ClayParams) -> Self" in lib_rs
+    assert "pub struct ClayParams { packed: u64 }" in lib_rs
+    for f in ("pub const fn n(&self) -> u8", "pub const fn k(&self) -> u8", "pub const fn d(&self) -> u8",
+              "pub const fn as_u64(&self) -> u64", "pub const fn from_u64(v: u64) -> Self"):
+        assert f in lib_rs, f
+    plan = re.search(r"pub struct RepairPlan \{(.*?)\n\}", hook, flags=re.S).group(1)
+    assert re.findall(r"pub (\w+):", plan) == ["lost", "num_stripes", "chunk_size", "sub_chunk_size", "stripes"]
+    assert "pub stripes: Vec<StripeRepair>" in plan
+    assert "pub struct StripeRepair { pub stripe: u32, pub lost_shard: SliceIndex, pub helpers: Vec<HelperPlan> }" in hook
+    assert "pub struct HelperPlan { pub slice: SliceIndex, pub shard: SliceIndex, pub sub_chunks: Vec<u32> }" in hook
+    # the pool is bounded (ADVICE r05 low)
+    assert "pub const KEEP: usize = 2;" in lib_rs
