@@ -691,11 +691,11 @@ def main():
                        + f" of {nobj} x {L} B objects per GPU, Clay(20,7,16) rotated, 1 MB stripes",
                        "objects_per_gpu": nobj, "object_bytes": L, "profile": "clay(20,7,16)",
                        "parallelism": f"objects partitioned over {world} GPU(s)"},
-            "roofline": {"bound": "hbm", "achieved": rnd(achieved, 1), "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": rnd(rates["frac"], 4),
+            "roofline": {"bound": "hbm", "achieved": rnd_opt(achieved, 1), "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": rnd_opt(rates["frac"], 4),
                          "traffic": traffic,
                          "alg_bytes_per_launch": unit_bytes * nobj if unit_bytes else None,
-                         "avg_launch_ms": rnd(rates["avg_launch_ms"], 4),
+                         "avg_launch_ms": rnd_opt(rates["avg_launch_ms"], 4),
                          "box_ceiling": ceiling,
                          "box_ceiling_frac": round(achieved / ceiling["blocks_GBps"], 4)
                          if ceiling and achieved else None},
@@ -816,10 +816,10 @@ def config5_bench(args, torch, dist, world, rank, dev, np, T, batch):
             "rank_ms_per_step": [round(x, 3) for x in rates["rank_ms_per_step"]],
             "rank_kernel_ms_per_step": [round(x, 3) for x in rank_kms],
             "rank_pci": [pci_str(int(x)) for x in rank_pci],
-            "roofline": {"bound": "hbm", "achieved": rnd(rates["achieved"], 1), "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": rnd(rates["frac"], 4),
+            "roofline": {"bound": "hbm", "achieved": rnd_opt(rates["achieved"], 1), "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": rnd_opt(rates["frac"], 4),
                          "traffic": None, "alg_bytes_per_launch": ALG_BYTES["encode"] * nb,
-                         "avg_launch_ms": rnd(rates["avg_launch_ms"], 4)},
+                         "avg_launch_ms": rnd_opt(rates["avg_launch_ms"], 4)},
             "cpu_baseline": cpu, "gpu": gpu_env(torch, dev),
             "copy_inclusive": {"value": round(total * L / max(c_rank) / 2**30, 3), "unit": "GiB/s", "pinned": True,
                                "host_ring_objects": ring, "rank_ms": [round(x * 1e3, 1) for x in c_rank],
@@ -831,7 +831,7 @@ def config5_bench(args, torch, dist, world, rank, dev, np, T, batch):
         dist.destroy_process_group()
 
 
-def rnd(x, nd):
+def rnd_opt(x, nd):
     return None if x is None else round(x, nd)
 
 

@@ -29,6 +29,7 @@
 #include "rs16.hpp"
 #include "host_hash.hpp"
 #include "copy_pool.hpp"
+#include "dec_class.hpp"
 
 using namespace tec;
 
@@ -519,6 +520,11 @@ struct te_clay {
     // CUs, slot streams (copies, encodes) on the rest
     hipStream_t cm_ss[2] = {}, cm_hs = nullptr;
     bool cm_tried = false;
+    // decode class kernels run side by side (decode_enqueue): side streams forked from and joined
+    // back into the call's stream with events, so their work is ordered like the call's
+    static constexpr int kClsSide = 3;
+    hipStream_t cls_s[kClsSide] = {};
+    hipEvent_t cls_fork = nullptr, cls_join[kClsSide] = {};
 };
 
 // Drain and free everything a handle holds on its device (on that device).
@@ -530,6 +536,10 @@ static void release_device_state(te_clay *c) {
     if (c->rec_done) (void)hipEventSynchronize(c->rec_done);
     for (auto &sl : c->pipe)
         if (sl.s) (void)hipStreamSynchronize(sl.s);
+    for (hipStream_t &cs : c->cls_s)
+        if (cs) (void)hipStreamSynchronize(cs), (void)hipStreamDestroy(cs), cs = nullptr;
+    for (hipEvent_t *pe : {&c->cls_fork, &c->cls_join[0], &c->cls_join[1], &c->cls_join[2]})
+        if (*pe) (void)hipEventDestroy(*pe), *pe = nullptr;
     c->enc.release();
     c->dec.release();
     c->rep.release();
@@ -1385,6 +1395,42 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
             kv.second.swap(rest);
         }
     }
+    // decode class kernels (decode_class.hip, dec_class.hpp): the remaining stripes of every
+    // Clay(20,7,16) survivor set run the ahead-of-time kernel of the set's class -- the program's
+    // control compiled in, the set's slices, planes and decoding matrix read at run time.
+    // Measurement option TEC_DEBUG_KNOBS=1 TEC_DEC_CLASS=0: the table-driven kernel instead.
+    struct ClassGrp { uint64_t key; int id; std::vector<GpeJob> jobs; size_t off = 0; };
+    std::vector<ClassGrp> cls;
+    static const bool class_on = [] {
+        const char *e = tec_knob("TEC_DEC_CLASS");
+        return !(e && e[0] == '0');
+    }();
+    if (staged && !fused && class_on) {
+        std::vector<int> cid(cached.size(), -1);
+        for (size_t p = 0; p < cached.size(); p++) {
+            const int id = dec_class_of(h, cached[p]->P);
+            cid[p] = id >= 0 && dec_class_info(id, nullptr, nullptr) ? id : -1;
+        }
+        for (auto &kv : groups) {
+            if (!staged_group(kv.first)) continue;
+            int at[kDecClasses];
+            std::fill(at, at + kDecClasses, -1);
+            std::vector<GpeJob> rest;
+            for (const GpeJob &g : kv.second) {
+                const int id = cid[g.pattern];
+                if (id < 0) {
+                    rest.push_back(g);
+                    continue;
+                }
+                if (at[id] < 0) {
+                    at[id] = (int)cls.size();
+                    cls.push_back(ClassGrp{kv.first, id, {}});
+                }
+                cls[(size_t)at[id]].jobs.push_back(g);
+            }
+            kv.second.swap(rest);
+        }
+    }
     // staged patterns live in the device store (uploaded once per handle), the jobs name slots;
     // otherwise (generic kernel, or more patterns than the store holds) they go in the arena
     std::vector<uint32_t> slot_of;
@@ -1396,9 +1442,12 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         int rs = TE_OK;
         in_store = dec_store_slots(c, cached, pat_keys, slot_of, fill, rs);
         if (rs) return rs;
-        if (in_store)
+        if (in_store) {
             for (auto &kv : groups)
                 for (GpeJob &g : kv.second) g.pattern = slot_of[g.pattern];
+            for (ClassGrp &cg : cls)
+                for (GpeJob &g : cg.jobs) g.pattern = slot_of[g.pattern];
+        }
     }
     std::vector<DecProgHdr> dhdrs;
     std::vector<DecStepP> dsteps;
@@ -1430,6 +1479,7 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     for (auto &kv : groups)
         if (!kv.second.empty()) offs.push_back({kv.first, A.put(kv.second.data(), kv.second.size() * sizeof(GpeJob))});
     for (Fixed &f : fixed) f.off = A.put(f.jobs.data(), f.jobs.size() * sizeof(GpeJob));
+    for (ClassGrp &cg : cls) cg.off = A.put(cg.jobs.data(), cg.jobs.size() * sizeof(GpeJob));
     // new store entries ride in the same upload, then move to their slots on this stream
     size_t fp_off = 0, fh_off = 0, fs_off = 0, fo_off = 0;
     if (in_store && !fill.pats.empty()) {
@@ -1473,6 +1523,8 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     }();
     size_t call_stripes = 0;
     for (auto &o : offs) call_stripes += groups[o.first].size();
+    for (const ClassGrp &cg : cls) call_stripes += cg.jobs.size();
+    const uint32_t class_g = call_stripes <= dec_small_max ? 1u : 2u;
     const bool small_dec = call_stripes <= dec_small_max;
     auto dec_args = [&](const std::pair<uint64_t, size_t> &o) {
         const uint64_t cs = o.first >> 32;
@@ -1525,15 +1577,63 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         const size_t b = (size_t)a.njobs * a.wgs_per_stripe * std::max(a.nscratch, 1u) * geo.G * 64u * geo.wb;
         scratch_bytes = std::max(scratch_bytes, b);
     }
+    // the class launches may run side by side: each its own scratch range, after the others'
+    size_t cls_bytes = 0;
+    for (const ClassGrp &cg : cls) {
+        const uint32_t sc = (uint32_t)((cg.key >> 32) / (uint64_t)h.alpha);
+        cls_bytes += dec_class_scratch_bytes(cg.id, (uint32_t)cg.jobs.size(), sc, class_g);
+    }
+    const size_t cls_off = (scratch_bytes + 255) & ~(size_t)255;
+    if (cls_bytes) scratch_bytes = cls_off + cls_bytes;
     uint8_t *scratch = nullptr;
     if (scratch_bytes) {
         r = A.workspace(scratch_bytes, s, &scratch);
         if (r) return r;
     }
+    uint8_t *const cls_scratch = scratch ? scratch + cls_off : nullptr;
     KTimer kt(s);
     for (const Fixed &f : fixed) {
         const dfix_args a = fixed_args(f, scratch);
         TE_HIP(launch_dec_fixed(*f.k, a, dec_jit_geom(a.sc).G, s));
+    }
+    if (!cls.empty()) {
+        // the class groups side by side on up to 1 + kClsSide streams, largest first, each with
+        // its own scratch range: one class's launch has a 100-step chain as its floor whatever
+        // its size, so groups one after another leave the GPU idle at every tail
+        static const int nstreams = [] {
+            const char *e = tec_knob("TEC_DEC_CLASS_STREAMS");
+            const int v = e ? atoi(e) : 1 + te_clay::kClsSide;
+            return std::max(1, std::min(v, 1 + te_clay::kClsSide));
+        }();
+        const int ns = std::min<int>(nstreams, (int)cls.size());
+        std::vector<size_t> order(cls.size());
+        for (size_t i = 0; i < order.size(); i++) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return cls[x].jobs.size() > cls[y].jobs.size(); });
+        hipStream_t ss[1 + te_clay::kClsSide] = {s};
+        if (ns > 1) {
+            if (!c->cls_fork) TE_HIP(hipEventCreateWithFlags(&c->cls_fork, hipEventDisableTiming));
+            TE_HIP(hipEventRecord(c->cls_fork, s));
+            for (int i = 1; i < ns; i++) {
+                if (!c->cls_s[i - 1]) TE_HIP(hipStreamCreateWithFlags(&c->cls_s[i - 1], hipStreamNonBlocking));
+                if (!c->cls_join[i - 1]) TE_HIP(hipEventCreateWithFlags(&c->cls_join[i - 1], hipEventDisableTiming));
+                TE_HIP(hipStreamWaitEvent(c->cls_s[i - 1], c->cls_fork, 0));
+                ss[i] = c->cls_s[i - 1];
+            }
+        }
+        const GpePattern *pp = in_store ? c->dstore.pats.as<GpePattern>() : A.at<GpePattern>(pat_off);
+        size_t scr_at = 0;
+        for (size_t k = 0; k < order.size(); k++) {
+            const ClassGrp &cg = cls[order[k]];
+            const uint64_t cs = cg.key >> 32;
+            const uint32_t sc = (uint32_t)(cs / (uint64_t)h.alpha);
+            TE_HIP(launch_dec_class(cg.id, A.at<GpeJob>(cg.off), pp, (uint32_t)cg.jobs.size(), sc, group_in_stride[cg.key],
+                                    cs, (uint32_t)n, cls_scratch + scr_at, class_g, ss[k % (size_t)ns]));
+            scr_at += dec_class_scratch_bytes(cg.id, (uint32_t)cg.jobs.size(), sc, class_g);
+        }
+        for (int i = 1; i < ns; i++) {
+            TE_HIP(hipEventRecord(c->cls_join[i - 1], ss[i]));
+            TE_HIP(hipStreamWaitEvent(s, c->cls_join[i - 1], 0));
+        }
     }
     for (auto &o : offs) {
         if (staged_group(o.first)) {

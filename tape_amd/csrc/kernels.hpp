@@ -238,6 +238,15 @@ DecJitGeom dec_jit_geom(uint32_t sc);
 hipError_t launch_dec_fixed(const DecJitKernel &k, const dfix_args &a, uint32_t G, hipStream_t s);
 bool decode_stage_k(int k);  // a staged-decode kernel is compiled for this k (n = 20)
 
+// Decode class kernels (decode_class.hip, dec_class.hpp): one ahead-of-time kernel per class of
+// 7-of-20 survivor sets of Clay(20,7,16), run-time node / plane relabelling and decoding matrix.
+bool dec_class_info(int id, uint32_t *nslots, uint32_t *nscratch);  // false: no such kernel
+uint32_t dec_class_wgs(uint32_t sc, uint32_t G);
+size_t dec_class_scratch_bytes(int id, uint32_t njobs, uint32_t sc, uint32_t G);
+hipError_t launch_dec_class(int id, const GpeJob *jobs, const GpePattern *patterns, uint32_t njobs, uint32_t sc,
+                            uint64_t in_stride, uint64_t out_stride, uint32_t n, uint8_t *scratch, uint32_t G,
+                            hipStream_t s);
+
 // ---- slice commitments (commit.hip) ----
 constexpr int kCommitMaxLeaves = 64;
 struct CommitArgs {
