@@ -146,13 +146,18 @@ struct ClayHost {
     // out_node >= 0: the output is that one node's chunk, item x = 0 (node recover's lost slice,
     // recover.rs:411-442: a parity node's C comes out of the same layered decode, so nothing is
     // re-encoded); pairs of erased nodes neither of which is output are skipped either way.
-    bool dec_prog(const GpePattern &P, int orient, DecProgHdr &H, std::vector<DecStep> &out, int out_node = -1) const {
+    // out_mask != 0 (decode class kernels): the output nodes are exactly those of the mask (items
+    // keep their node ids); the kernel drops the outputs that are not data rows.
+    bool dec_prog(const GpePattern &P, int orient, DecProgHdr &H, std::vector<DecStep> &out, int out_node = -1,
+                  uint64_t out_mask = 0) const {
         if (q != kRepQ || t != 2 || nu != 0 || alpha != kRepQ * kRepQ) return false;
         if (P.nknown > (uint32_t)kDecMaxK || P.nerased > (uint32_t)kDecMaxE) return false;
         const uint64_t em = P.erased_mask;
         auto er = [&](int node) { return ((em >> node) & 1ull) != 0; };
-        auto isdata = [&](int node) { return out_node < 0 ? node < k : node == out_node; };  // an output node
-        const uint32_t relabel = out_node < 0 ? 0xffu : 0u;
+        auto isdata = [&](int node) {  // an output node
+            return out_mask ? ((out_mask >> node) & 1ull) != 0 : out_node < 0 ? node < k : node == out_node;
+        };
+        const uint32_t relabel = out_node < 0 || out_mask ? 0xffu : 0u;
         const int yo = orient ? 1 : 0, yi = 1 - yo;
         std::vector<int> rows, cols;
         for (int pass = 0; pass < 2; pass++)
@@ -193,7 +198,7 @@ struct ClayHost {
             for (int i = 0; i < kDecMaxK; i++) S.kk[i] = kKnRed, S.kp[i] = 0, S.kout[i] = kLocNone;
             for (int i = 0; i < kDecMaxE; i++) S.ek[i] = kErSkip, S.ep[i] = 0, S.ed0[i] = S.ed1[i] = S.epd[i] = kLocNone;
             auto add_out = [&](int node, int plane) -> uint32_t {
-                if (S.nout >= (uint32_t)kDecMaxOut) return kLocNone;
+                if (S.nout >= (uint32_t)kDecMaxOutProg) return kLocNone;
                 S.out[S.nout] = (relabel == 0xffu ? (uint32_t)node : relabel) | ((uint32_t)plane << 8);
                 return (kLocStage << 24) | S.nout++;
             };
@@ -340,6 +345,12 @@ struct ClayHost {
         for (size_t i = 0; i < erased.size(); i++) P.erased[i] = (uint8_t)erased[i];
         for (size_t e = 0; e < erased.size(); e++)
             for (size_t j = 0; j < known.size(); j++) P.D[e][j] = perm_tab(D.v[e][j]);
+        if (erased.size() <= (size_t)kClsMaxE && known.size() <= (size_t)kClsMaxK)
+            for (size_t e = 0; e < erased.size(); e++)
+                for (size_t j = 0; j < known.size(); j++) {
+                    const PermTab4 t = perm_tab4(D.v[e][j]);
+                    for (int f = 0; f < 4; f++) P.D4[e][j][f] = t.t[f];
+                }
         std::vector<int> score(alpha, 0);
         int maxs = 0;
         for (int z = 0; z < alpha; z++) {

@@ -5,20 +5,23 @@
 // Clay(20,7,16) sees any 7 of the 20 slices: 77,520 survivor sets, each with its own layered-decode
 // plane program.  The coupling structure of q = 10, t = 2 is invariant under relabelling the x
 // digit of each column (a permutation pi_y of column y's nodes applied to plane digit z_y as well,
-// A4: the PFT is symmetric), so two survivor sets related by such a relabelling have isomorphic
-// programs.  Slicer::decode outputs the data nodes (0..6, all in column 0), so the relabellings
-// that keep data nodes data nodes are S7 x S3 on column 0 and S10 on column 1.  Their orbits on
-// 7-of-20 survivor sets are indexed by (a, b, c): a known data nodes, b known column-0 parity
-// nodes (7..9), c known column-1 nodes, a + b + c = 7 -- 26 classes.
+// A4: the PFT is symmetric), so survivor sets related by such a relabelling have isomorphic
+// programs.  The class programs output every erased node of column 0 -- the data nodes 0..6 and
+// the column-0 parity nodes 7..9 alike (dec_prog's out_mask) -- and the kernel drops the stores
+// of the parity ones, so the relabellings are all of S10 x S10 and the classes are indexed by a0,
+// the number of known column-0 nodes (0..7; the rest of the 7 are in column 1): 8 classes.
+// Treating the three column-0 parity nodes as outputs costs ~5 % more MDS products (weighted over
+// all survivor sets; 0 - 16 % by class) and saves the launches that 26 data-only classes needed
+// (one launch's floor is a stripe's 100-step chain, whatever its size).
 //
-// The representative of class (a, b, c) keeps nodes {0..a-1, 7..7+b-1, 10..10+c-1}.  Its program
+// The representative of class a0 keeps nodes {0..a0-1} and {10..10+(7-a0)-1}.  Its program
 // (ClayHost::dec_prog) is written out as straight-line code once, at build time, with every node
 // and plane symbolic: canonical known node j is the pattern's known[j], canonical erased node e
 // its erased[e] (both lists ascending, and the relabelling is monotone on the known and on the
-// erased nodes of each group, so the pattern's own decoding matrix D[e][j] is already in canonical
-// order), canonical plane (z0, z1) is physical plane (pi_0(z0), pi_1(z1)).  At run time a kernel
-// reads the pattern's node lists and decoding matrix (the device pattern store, as the table
-// kernel does) and turns them into slice offsets and plane offsets once per workgroup; the
+// erased nodes of each column, so the pattern's own decoding matrix D[e][j] is already in
+// canonical order), canonical plane (z0, z1) is physical plane (pi_0(z0), pi_1(z1)).  At run time
+// a kernel reads the pattern's node lists and decoding matrix (the device pattern store, as the
+// table kernel does) and turns them into slice offsets and plane offsets once per workgroup; the
 // program's control -- which loads, which products, where each value goes -- is compile-time.
 // Products stay run-time v_perm table products (the matrix belongs to the survivor set).
 #pragma once
@@ -29,52 +32,65 @@
 
 namespace tec {
 
-constexpr int kDecClassN = 20, kDecClassK = 7, kDecClasses = 26;
-constexpr uint32_t kDecClassNone = 0xffffffffu;
+// Classes 0..7: Slicer::decode, a0 known column-0 nodes.  Classes 8..23: node recover
+// (recover.rs:411-442, dec_prog's out_node), 8 + 2 a0 + yL: the lost node is in column yL.  For
+// recover the one output is the lost node, so data and parity nodes are alike and the same S10 x
+// S10 relabellings apply once the lost node is fixed: the pattern's erased list puts the lost node
+// first among its column's erased nodes (dec_class_lost_first, with the matrix rows), and the
+// representative's lost node is the first erased node of column yL.
+constexpr int kDecClassN = 20, kDecClassK = 7, kDecClassesDecode = 8, kDecClasses = 24;
+constexpr uint64_t kDecClassOutMask = 0x3ffull;  // decode: every column-0 node is an output
 
 struct DecClassSpec {
-    int a, b, c;  // known data nodes, known column-0 parity nodes, known column-1 nodes
+    int a0;  // known column-0 nodes (the other 7 - a0 known nodes are in column 1)
+    int yl;  // recover: the lost node's column; -1 for decode
 };
 
 inline DecClassSpec dec_class_spec(int id) {
-    int i = 0;
-    for (int b = 0; b <= 3; b++)
-        for (int a = 0; a + b <= 7; a++, i++)
-            if (i == id) return DecClassSpec{a, b, 7 - a - b};
-    return DecClassSpec{-1, -1, -1};
-}
-
-inline int dec_class_index(int a, int b) {
-    int i = 0;
-    for (int bb = 0; bb <= 3; bb++)
-        for (int aa = 0; aa + bb <= 7; aa++, i++)
-            if (aa == a && bb == b) return i;
-    return -1;
+    if (id < 0 || id >= kDecClasses) return DecClassSpec{-1, -1};
+    if (id < kDecClassesDecode) return DecClassSpec{id, -1};
+    return DecClassSpec{(id - kDecClassesDecode) / 2, (id - kDecClassesDecode) % 2};
 }
 
 // The class of a padded pattern of Clay(20,7,16) (internal ids = node ids, nu = 0), or -1.
-inline int dec_class_of(const ClayHost &h, const GpePattern &P) {
+// lost >= 0: the recover class of (P, lost node), P's erased list already lost-first.
+inline int dec_class_of(const ClayHost &h, const GpePattern &P, int lost = -1) {
     if (h.n != kDecClassN || h.k != kDecClassK || h.q != kRepQ || h.t != 2 || h.nu != 0) return -1;
     if (P.nknown != (uint32_t)kDecClassK || P.nerased != (uint32_t)(kDecClassN - kDecClassK)) return -1;
-    int a = 0, b = 0;
-    for (uint32_t j = 0; j < P.nknown; j++) {
-        a += P.known[j] < 7;
-        b += P.known[j] >= 7 && P.known[j] < 10;
+    int a0 = 0;
+    for (uint32_t j = 0; j < P.nknown; j++) a0 += P.known[j] < 10;
+    if (lost < 0) return a0;
+    if (lost >= kDecClassN || !((P.erased_mask >> lost) & 1ull)) return -1;
+    const int yl = lost / 10;
+    const uint32_t first = yl == 0 ? 0u : (uint32_t)(10 - a0);  // the lost node's place in the erased list
+    if (P.erased[first] != (uint32_t)lost) return -1;
+    return kDecClassesDecode + 2 * a0 + yl;
+}
+
+// Put the lost node first among its column's erased nodes (P.erased and the matrix rows D, D4),
+// the order the recover class kernels' relabelling assumes.  Every program compiled from P after
+// this follows the same order.
+inline void dec_class_lost_first(GpePattern &P, int lost) {
+    int at = -1, first = -1;
+    for (uint32_t e = 0; e < P.nerased; e++) {
+        if ((int)P.erased[e] == lost) at = (int)e;
+        if (first < 0 && (int)P.erased[e] / 10 == lost / 10) first = (int)e;
     }
-    return dec_class_index(a, b);
+    if (at < 0 || first < 0 || at == first) return;
+    for (int e = at; e > first; e--) {  // rotate [first, at] right by one
+        std::swap(P.erased[e], P.erased[e - 1]);
+        for (int j = 0; j < kGpeMaxKnown; j++) std::swap(P.D[e][j], P.D[e - 1][j]);
+        if (e < kClsMaxE)
+            for (int j = 0; j < kClsMaxK; j++)
+                for (int f = 0; f < 4; f++) std::swap(P.D4[e][j][f], P.D4[e - 1][j][f]);
+    }
 }
 
 // Canonical node c of class s: (known?, index into the pattern's known / erased list).
 inline std::pair<bool, int> dec_class_slot(const DecClassSpec &s, int c) {
-    if (c < 10) {
-        if (c < s.a) return {true, c};
-        if (c < 7) return {false, c - s.a};
-        if (c < 7 + s.b) return {true, s.a + (c - 7)};
-        return {false, (7 - s.a) + (c - 7 - s.b)};
-    }
-    const int r = c - 10;
-    if (r < s.c) return {true, s.a + s.b + r};
-    return {false, (7 - s.a) + (3 - s.b) + (r - s.c)};
+    if (c < 10) return c < s.a0 ? std::make_pair(true, c) : std::make_pair(false, c - s.a0);
+    const int r = c - 10, c1 = kDecClassK - s.a0;
+    return r < c1 ? std::make_pair(true, s.a0 + r) : std::make_pair(false, (10 - s.a0) + (r - c1));
 }
 
 inline uint64_t dec_class_emask(const DecClassSpec &s) {
@@ -84,19 +100,24 @@ inline uint64_t dec_class_emask(const DecClassSpec &s) {
     return m;
 }
 
-// Program of class `id`'s representative, in the orientation decode_enqueue's table path prefers
-// (two workgroups per CU first, then fewer scratch rows).
+// Program of class `id`'s representative: of the two row orientations the one with fewer
+// scratch rows (HBM traffic), then fewer MDS rows (VALU), within the LDS of two workgroups per CU.
 inline bool dec_class_prog(const ClayHost &h, int id, GpePattern &P, DecProgHdr &H, std::vector<DecStep> &steps) {
     const DecClassSpec s = dec_class_spec(id);
     std::vector<uint16_t> pool;
-    if (s.a < 0 || !h.gpe_pattern(dec_class_emask(s), P, pool)) return false;
+    if (s.a0 < 0 || !h.gpe_pattern(dec_class_emask(s), P, pool)) return false;
     bool found = false;
+    uint64_t best = 0;
     for (int orient = 0; orient < 2; orient++) {
         DecProgHdr H1;
         std::vector<DecStep> st;
-        if (!h.dec_prog(P, orient, H1, st)) continue;
-        const auto cost = [](const DecProgHdr &x) { return (x.nslots + 2 > 53 ? 1u << 20 : 0u) + x.nscratch; };
-        if (!found || cost(H1) < cost(H)) { H = H1; steps.swap(st); found = true; }
+        const uint64_t out_mask = s.yl < 0 ? kDecClassOutMask : 1ull << (s.yl == 0 ? s.a0 : 10 + (kDecClassK - s.a0));
+        if (!h.dec_prog(P, orient, H1, st, -1, out_mask)) continue;
+        uint64_t rows = 0;
+        for (const DecStep &S : st)
+            for (uint32_t e = 0; e < P.nerased; e++) rows += S.ek[e] != kErSkip;
+        const uint64_t cost = (H1.nslots + 2 > 53 ? 1ull << 40 : 0ull) + ((uint64_t)H1.nscratch << 20) + rows;
+        if (!found || cost < best) { H = H1; steps.swap(st); best = cost; found = true; }
     }
     return found;
 }
@@ -106,7 +127,17 @@ inline size_t dec_class_lds(uint32_t nslots, int G) { return (size_t)(nslots ? n
 
 // Kernel source of class `id` (one translation unit; decode_class_dev.hpp has the helpers).
 // t_u: the type-1 coefficient (C = t_u (U ^ Cp) ^ Cp).
-inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecProgHdr &Hout) {
+// Generator options (build-time variants for A/B runs; the defaults are what the library ships):
+// wpe = the waves-per-SIMD register budget, late = a step's loads for the next step issued after
+// its products instead of at its start.
+struct DecClassGenOpt {
+    int wpe = 4;
+    bool late = false;
+    bool tab4 = true;  // 2-bit-field product tables (PermTab4); false: the 3/3/2-bit PermTab
+};
+
+inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecProgHdr &Hout,
+                                    const DecClassGenOpt &opt = DecClassGenOpt()) {
     GpePattern P;
     DecProgHdr H;
     std::vector<DecStep> steps;
@@ -132,18 +163,24 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
         const auto sl = dec_class_slot(cs, node);
         return sl.first ? sl.second : -1;
     };
-    emit("// generated by gen_dec_class (dec_class.hpp): class %d = (a %d, b %d, c %d), %d steps, %u slots, "
-         "%u scratch rows\n", id, cs.a, cs.b, cs.c, NS, H.nslots, H.nscratch);
+    emit("// generated by gen_dec_class (dec_class.hpp): class %d = %d known column-0 nodes, %s, %d steps, %u slots, "
+         "%u scratch rows\n", id, cs.a0, cs.yl < 0 ? "decode" : cs.yl == 0 ? "recover, lost node in column 0" :
+         "recover, lost node in column 1", NS, H.nslots, H.nscratch);
     s += "#include \"decode_class_dev.hpp\"\nnamespace tec {\nnamespace dcls {\n";
-    emit("template <int G>\n__global__ void __attribute__((amdgpu_flat_work_group_size(1, G * 64), amdgpu_waves_per_eu(4)))\n"
-         "dec_class_%d(DecClassArgs a) {\n", id);
+    emit("template <int G>\n__global__ void __attribute__((amdgpu_flat_work_group_size(1, G * 64), amdgpu_waves_per_eu(%d)))\n"
+         "dec_class_%d(DecClassArgs a) {\n", opt.wpe, id);
     s += "  extern __shared__ __attribute__((aligned(16))) u32 lds[];\n  CTile<G> T(a, reinterpret_cast<u8 *>(lds));\n";
     // per-workgroup offsets: known slices, plane digits, data chunks (only what the program uses;
     // the rest is dead code)
     for (int j = 0; j < NK; j++) emit("  const u32 kb%d = T.kbase(T.K(%d));\n", j, j);
     for (int x = 0; x < 10; x++) emit("  const u32 pz0_%d = %s * 10u * T.sc;\n", x, phys(x).c_str());
     for (int x = 0; x < 10; x++) emit("  const u32 pz1_%d = (%s - 10u) * T.sc;\n", x, phys(10 + x).c_str());
-    for (int x = 0; x < kDecClassK; x++) emit("  const u32 ob%d = %s * T.out_stride;\n", x, phys(x).c_str());
+    // decode: column-0 outputs, a data chunk or dropped (a parity node: an offset past the range);
+    // recover: the lost node's chunk is the job's whole output
+    if (cs.yl < 0)
+        for (int x = 0; x < 10; x++) emit("  const u32 ob%d = T.out_base(%s);\n", x, phys(x).c_str());
+    else
+        emit("  const u32 ob%d = 0u;\n", cs.yl == 0 ? cs.a0 : 10 + (kDecClassK - cs.a0));
     auto poff = [&](uint32_t z) {
         return "pz0_" + std::to_string(z / 10) + " + pz1_" + std::to_string(z % 10);
     };
@@ -185,7 +222,7 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
             }
         };
         emit("  // step %d: plane (%u, %u)\n", st, S.z / 10, S.z % 10);
-        loads(st + 1);
+        if (!opt.late) loads(st + 1);
         // uncouple the known nodes (known data rows are copied out as they are)
         for (int j = 0; j < NK; j++) {
             const std::string id = id2(st, j);
@@ -207,11 +244,12 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
         bool any = false;
         for (int e = 0; e < NE; e++) any = any || S.ek[e] != kErSkip;
         if (any) {
-            for (int j = 0; j < NK; j++) emit("  const Sel s%s(u%s);\n", id2(st, j).c_str(), id2(st, j).c_str());
+            for (int j = 0; j < NK; j++)
+                emit("  const %s s%s(u%s);\n", opt.tab4 ? "Sel4" : "Sel", id2(st, j).c_str(), id2(st, j).c_str());
             for (int e = 0; e < NE; e++) {
                 if (S.ek[e] == kErSkip) continue;
                 const std::string a = "a" + id2(st, e);
-                emit("  u32 %s = 0u;\n  { const auto D = T.mat();\n", a.c_str());
+                emit("  u32 %s = 0u;\n  { const auto D = T.%s();\n", a.c_str(), opt.tab4 ? "mat4" : "mat");
                 for (int j = 0; j + 1 < NK; j += 2)
                     emit("  %s = T.mul2(%s, D, %d, %d, s%s, s%s);\n", a.c_str(), a.c_str(), e, j, id2(st, j).c_str(),
                          id2(st, j + 1).c_str());
@@ -244,6 +282,7 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
                 }
             }
         }
+        if (opt.late) loads(st + 1);
         scr_loads(st + 1);
     }
     s += "}\n";

@@ -41,6 +41,7 @@ size_t dec_class_scratch_bytes(int id, uint32_t njobs, uint32_t sc, uint32_t G) 
 hipError_t launch_dec_class(int id, const GpeJob *jobs, const GpePattern *patterns, uint32_t njobs, uint32_t sc,
                             uint64_t in_stride, uint64_t out_stride, uint32_t n, uint8_t *scratch, uint32_t G,
                             hipStream_t s) {
+    const DecClassSpec spec = dec_class_spec(id);
     if (njobs == 0) return hipSuccess;
     uint32_t nslots = 0, nscr = 0;
     if (!dec_class_info(id, &nslots, &nscr) || (G != 1 && G != 2) || sc < 8 || n != (uint32_t)kDecClassN)
@@ -57,6 +58,9 @@ hipError_t launch_dec_class(int id, const GpeJob *jobs, const GpePattern *patter
     a.wgs_per_stripe = dec_class_wgs(sc, G);
     a.n = n;
     a.nscratch = nscr;
+    // decode writes the k data chunks of a stripe, recover the lost node's one chunk
+    const uint64_t full = spec.yl < 0 ? (uint64_t)kDecClassK * out_stride : out_stride;
+    a.out_full = full > 0xffffffffull ? 0xffffffffu : (uint32_t)full;
     const uint64_t blocks = (uint64_t)njobs * a.wgs_per_stripe;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     const size_t lds = dec_class_lds(nslots, (int)G);

@@ -26,6 +26,7 @@ struct DecClassArgs {
     u64 in_stride;               // slice length
     u64 out_stride;              // chunk size
     u32 njobs, sc, wps, wgs_per_stripe, n, nscratch;
+    u32 out_full;                // a job whose out_len reaches this writes every output row whole
 };
 
 // host registry entry of one class (decode_class.hip)
@@ -44,6 +45,7 @@ struct CTile {
     u8 *lds8;
     cPat *pat;
     u32 lane, col_local, vcol, sc, olen, rot, n, in_stride, out_stride;
+    bool full;
     __amdgpu_buffer_rsrc_t rs_in, rs_out, rs_scr;
 
     __device__ __forceinline__ CTile(const DecClassArgs &a, u8 *lds) {
@@ -66,6 +68,7 @@ struct CTile {
         vcol = col + 4u > a.sc ? a.sc - 4u : col;  // the row's last 4 bytes for a word past the sub-chunk
         rs_in = __builtin_amdgcn_make_buffer_rsrc((void *)J.in, 0, (int)(u32)(a.n * a.in_stride), 0x00020000);
         olen = (u32)J.out_len;
+        full = olen >= a.out_full;  // every output row inside the job's output share (not a last stripe)
         rs_out = __builtin_amdgcn_make_buffer_rsrc((void *)J.out, 0, (int)olen, 0x00020000);
         const u32 nscr = a.nscratch ? a.nscratch : 1u;
         rs_scr = __builtin_amdgcn_make_buffer_rsrc(a.scratch + (u64)tile * nscr * RS, 0, (int)(nscr * RS), 0x00020000);
@@ -93,11 +96,17 @@ struct CTile {
     __device__ __forceinline__ void scr_st(u32 row, u32 v) const {
         __builtin_amdgcn_raw_buffer_store_b32(v, rs_scr, (int)col_local, (int)(row * RS), 0);
     }
+    // output base of column-0 node `node`: its data chunk, or for a parity node an offset past
+    // every stripe's output range, so the buffer range check drops its stores
+    __device__ __forceinline__ u32 out_base(u32 node) const { return node < kData ? node * out_stride : kDropBase; }
+    static constexpr u32 kData = 7, kDropBase = 0x80000000u;
     // one decoded word to data chunk offset `ob` at plane offset `po`, where it was loaded; a
     // word across the end of the stripe's output share is written byte by byte
     __device__ __forceinline__ void out_st(u32 ob, u32 po, u32 v) const {
         const u32 o = ob + po + vcol;
-        if (o + 4u > olen && o < olen) {
+        if (full) {  // uniform: every data row of the stripe lies inside its output share
+            __builtin_amdgcn_raw_buffer_store_b32(v, rs_out, (int)o, 0, 2);
+        } else if (o + 4u > olen && o < olen) {
 #pragma unroll
             for (u32 k = 0; k < 4u; k++) __builtin_amdgcn_raw_buffer_store_b8((u8)(v >> (8u * k)), rs_out, (int)(o + k), 0, 0);
         } else {
@@ -112,6 +121,22 @@ struct CTile {
         asm volatile("; mat" : "+s"(p));
         pat = (cPat *)(uintptr_t)p;
         return pat->D;
+    }
+    // the 2-bit-field tables of one erased row (laundered as mat())
+    typedef const __attribute__((address_space(4))) u32 cU32;
+    __device__ __forceinline__ cU32 (*mat4())[kClsMaxK][4] {
+        u64 p = (u64)(uintptr_t)pat;
+        asm volatile("; mat4" : "+s"(p));
+        pat = (cPat *)(uintptr_t)p;
+        return pat->D4;
+    }
+    __device__ __forceinline__ static u32 mul2(u32 acc, cU32 (*D)[kClsMaxK][4], int e, int j, const Sel4 &x, const Sel4 &y) {
+        cU32 *p = D[e][j], *q = D[e][j + 1];
+        return perm4_mul2_acc(acc, x, p[0], p[1], p[2], p[3], y, q[0], q[1], q[2], q[3]);
+    }
+    __device__ __forceinline__ static u32 mul1(u32 acc, cU32 (*D)[kClsMaxK][4], int e, int j, const Sel4 &x) {
+        cU32 *p = D[e][j];
+        return perm4_mul_acc(acc, x, p[0], p[1], p[2], p[3]);
     }
     __device__ __forceinline__ static u32 mul2(u32 acc, cTab (*D)[kGpeMaxKnown], int e, int j, const Sel &x, const Sel &y) {
         cTab &p = D[e][j], &q = D[e][j + 1];

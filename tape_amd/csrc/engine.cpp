@@ -522,7 +522,7 @@ struct te_clay {
     bool cm_tried = false;
     // decode class kernels run side by side (decode_enqueue): side streams forked from and joined
     // back into the call's stream with events, so their work is ordered like the call's
-    static constexpr int kClsSide = 3;
+    static constexpr int kClsSide = 7;
     hipStream_t cls_s[kClsSide] = {};
     hipEvent_t cls_fork = nullptr, cls_join[kClsSide] = {};
 };
@@ -538,8 +538,9 @@ static void release_device_state(te_clay *c) {
         if (sl.s) (void)hipStreamSynchronize(sl.s);
     for (hipStream_t &cs : c->cls_s)
         if (cs) (void)hipStreamSynchronize(cs), (void)hipStreamDestroy(cs), cs = nullptr;
-    for (hipEvent_t *pe : {&c->cls_fork, &c->cls_join[0], &c->cls_join[1], &c->cls_join[2]})
-        if (*pe) (void)hipEventDestroy(*pe), *pe = nullptr;
+    if (c->cls_fork) (void)hipEventDestroy(c->cls_fork), c->cls_fork = nullptr;
+    for (hipEvent_t &pe : c->cls_join)
+        if (pe) (void)hipEventDestroy(pe), pe = nullptr;
     c->enc.release();
     c->dec.release();
     c->rep.release();
@@ -1111,6 +1112,9 @@ bool compile_pattern(const ClayHost &h, uint64_t emask, int out_node, te_clay::D
     const int n = h.n;
     if (!h.gpe_pattern(emask, d.P, d.planes)) return false;
     d.P.planes_off = 0;
+    // node recover of Clay(20,7,16): the lost node first among its column's erased nodes, the
+    // order the recover class kernels assume (dec_class.hpp); every program below follows it
+    if (out_node >= 0 && dec_class_of(h, d.P) >= 0) dec_class_lost_first(d.P, out_node);
     // staged kernel (decode_stage.hip): compiled per k with every other node erased (padded
     // patterns); of the two row orientations, two workgroups per CU first (2 x 53 x 1536 B <=
     // 160 KB), then fewer scratch rows
@@ -1405,10 +1409,17 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         const char *e = tec_knob("TEC_DEC_CLASS");
         return !(e && e[0] == '0');
     }();
-    if (staged && !fused && class_on) {
+    // streams the class groups of a call run on, side by side (TEC_DEC_CLASS_STREAMS)
+    static const int class_streams = [] {
+        const char *e = tec_knob("TEC_DEC_CLASS_STREAMS");
+        const int v = e ? atoi(e) : 4;  // the process's hardware queues (GPU_MAX_HW_QUEUES default)
+        return std::max(1, std::min(v, 1 + te_clay::kClsSide));
+    }();
+    if (staged && class_on) {
         std::vector<int> cid(cached.size(), -1);
         for (size_t p = 0; p < cached.size(); p++) {
-            const int id = dec_class_of(h, cached[p]->P);
+            const int onode = (int)(pat_keys[p] >> 48) - 1;  // >= 0: node recover's output node
+            const int id = dec_class_of(h, cached[p]->P, onode);
             cid[p] = id >= 0 && dec_class_info(id, nullptr, nullptr) ? id : -1;
         }
         for (auto &kv : groups) {
@@ -1429,6 +1440,16 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
                 cls[(size_t)at[id]].jobs.push_back(g);
             }
             kv.second.swap(rest);
+        }
+        // a call that does not fill the GPU is bound by one stripe's 100-step chain per launch:
+        // with more class groups than streams some launches would run after others, so such a
+        // call runs on the table-driven kernel in one launch (per call 64 MiB: 3.67 ms as
+        // classes against 3.00, r06)
+        size_t ncls = 0;
+        for (const ClassGrp &cg : cls) ncls += cg.jobs.size();
+        if (cls.size() > (size_t)class_streams && ncls < 1024) {
+            for (ClassGrp &cg : cls) groups[cg.key].insert(groups[cg.key].end(), cg.jobs.begin(), cg.jobs.end());
+            cls.clear();
         }
     }
     // staged patterns live in the device store (uploaded once per handle), the jobs name slots;
@@ -1600,12 +1621,7 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         // the class groups side by side on up to 1 + kClsSide streams, largest first, each with
         // its own scratch range: one class's launch has a 100-step chain as its floor whatever
         // its size, so groups one after another leave the GPU idle at every tail
-        static const int nstreams = [] {
-            const char *e = tec_knob("TEC_DEC_CLASS_STREAMS");
-            const int v = e ? atoi(e) : 1 + te_clay::kClsSide;
-            return std::max(1, std::min(v, 1 + te_clay::kClsSide));
-        }();
-        const int ns = std::min<int>(nstreams, (int)cls.size());
+        const int ns = std::min<int>(class_streams, (int)cls.size());
         std::vector<size_t> order(cls.size());
         for (size_t i = 0; i < order.size(); i++) order[i] = i;
         std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return cls[x].jobs.size() > cls[y].jobs.size(); });

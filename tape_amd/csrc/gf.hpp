@@ -150,6 +150,18 @@ inline constexpr Pft kPft = make_pft();
 struct PermTab {
     uint32_t t[5];
 };
+// 2-bit fields: t[f] byte j = c * (j << 2f), j < 4 -- one dword per field, so a v_perm selects
+// from the same register twice (gfx9 reads one SGPR per VALU instruction: no v_mov needed)
+struct PermTab4 {
+    uint32_t t[4];
+};
+
+constexpr PermTab4 perm_tab4(uint8_t c) {
+    PermTab4 r{};
+    for (int f = 0; f < 4; f++)
+        for (int j = 0; j < 4; j++) r.t[f] |= (uint32_t)gf_mul(c, (uint8_t)(j << (2 * f))) << (8 * j);
+    return r;
+}
 constexpr PermTab perm_tab(uint8_t c) {
     PermTab r{};
     constexpr int sh[3] = {0, 3, 6}, n[3] = {8, 8, 4};

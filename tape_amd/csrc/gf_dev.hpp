@@ -89,6 +89,32 @@ __device__ __forceinline__ uint32_t perm_mul2_acc(uint32_t acc, const Sel &sx, u
     return gf_xor3(gf_xor3(acc, a, b), gf_xor3(c, d, e), f);
 }
 
+// 2-bit fields of four packed bytes (PermTab4 tables)
+struct Sel4 {
+    uint32_t s0, s1, s2, s3;
+    __device__ __forceinline__ Sel4() {}
+    __device__ __forceinline__ explicit Sel4(uint32_t x)
+        : s0(x & 0x03030303u), s1((x >> 2) & 0x03030303u), s2((x >> 4) & 0x03030303u), s3((x >> 6) & 0x03030303u) {}
+};
+
+// acc ^ c * x ^ d * y with 2-bit tables: eight v_perm (each reading one table dword twice, so the
+// tables stay in SGPRs with no move) and four XOR3
+__device__ __forceinline__ uint32_t perm4_mul2_acc(uint32_t acc, const Sel4 &x, uint32_t c0, uint32_t c1, uint32_t c2,
+                                                   uint32_t c3, const Sel4 &y, uint32_t d0, uint32_t d1, uint32_t d2,
+                                                   uint32_t d3) {
+    const uint32_t a = __builtin_amdgcn_perm(c0, c0, x.s0), b = __builtin_amdgcn_perm(c1, c1, x.s1);
+    const uint32_t c = __builtin_amdgcn_perm(c2, c2, x.s2), d = __builtin_amdgcn_perm(c3, c3, x.s3);
+    const uint32_t e = __builtin_amdgcn_perm(d0, d0, y.s0), f = __builtin_amdgcn_perm(d1, d1, y.s1);
+    const uint32_t g = __builtin_amdgcn_perm(d2, d2, y.s2), h = __builtin_amdgcn_perm(d3, d3, y.s3);
+    return gf_xor3(gf_xor3(gf_xor3(acc, a, b), c, d), gf_xor3(e, f, g), h);
+}
+__device__ __forceinline__ uint32_t perm4_mul_acc(uint32_t acc, const Sel4 &x, uint32_t c0, uint32_t c1, uint32_t c2,
+                                                  uint32_t c3) {
+    const uint32_t a = __builtin_amdgcn_perm(c0, c0, x.s0), b = __builtin_amdgcn_perm(c1, c1, x.s1);
+    const uint32_t c = __builtin_amdgcn_perm(c2, c2, x.s2), d = __builtin_amdgcn_perm(c3, c3, x.s3);
+    return gf_xor3(gf_xor3(acc, a, b), c, d);
+}
+
 __device__ __forceinline__ uint32_t perm_mul(const Sel &s, const PermTab &t) {
     return perm_mul(s, t.t[0], t.t[1], t.t[2], t.t[3], t.t[4]);
 }

@@ -75,7 +75,11 @@ struct GpePattern {
     uint32_t planes_off;               // offset (in uint16) of this pattern's plane list in the plane pool
     uint32_t pad_;
     PermTab D[kGpeMaxErased][kGpeMaxKnown];  // U_erased[e] = sum_j D[e][j] * U_known[j]
+    // the same matrix as 2-bit-field tables (perm_tab4) for patterns of at most kClsMaxE x kClsMaxK
+    // (the decode class kernels: each v_perm reads one table dword twice, so no table move)
+    uint32_t D4[13][7][4];
 };
+constexpr int kClsMaxE = 13, kClsMaxK = 7;
 
 struct GpeJob {
     const uint8_t *in;     // node-strided input base
@@ -144,6 +148,7 @@ struct RepProg {                   // 32-bit fields: scalar loads have no sub-dw
 // per-stripe global scratch row (later row).  Location codes: 0xffffffff none, else
 // type << 24 | index with type 0 staging row, 1 LDS slot, 2 scratch row.
 constexpr int kDecMaxK = 10, kDecMaxE = 13, kDecMaxOut = 16;
+constexpr int kDecMaxOutProg = 32;  // DecStep items: the packed (table-kernel) form holds kDecMaxOut
 constexpr uint32_t kLocNone = 0xffffffffu;
 enum : uint32_t { kLocStage = 0, kLocSlot = 1, kLocScratch = 2 };
 enum : uint32_t { kKnRed = 0, kKnInput = 1, kKnLoc = 2 };                       // known j kinds
@@ -151,7 +156,7 @@ enum : uint32_t { kErSkip = 0, kErRed = 1, kErType1 = 2, kErPark = 3, kErFinish 
 struct DecStep {
     uint32_t z;                    // plane
     uint32_t nout;                 // flush items (item i = staging row i)
-    uint32_t out[kDecMaxOut];      // data chunk x | plane << 8
+    uint32_t out[kDecMaxOutProg];  // data chunk x | plane << 8
     uint32_t kk[kDecMaxK];         // known j kind
     uint32_t kp[kDecMaxK];         // kKnInput: partner node | plane << 8; kKnLoc: partner C location
     uint32_t kout[kDecMaxK];       // staging row of the known node's C (data nodes), or none
