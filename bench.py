@@ -159,7 +159,7 @@ KERNELS = {
     "repair": ["tec::rfold::rep_fold_kernel"],  # every folded instance (lost column x known set)
     "decode": ["tec_dec_fixed"],  # the pattern kernels (dec_rtc.cpp); random patterns / --decode-jit off: table-driven
     "commit": ["tec::commit::leaf_kernel", "tec::commit::tree_kernel"],
-    "recover": ["tec::dstage::dec_stage_kernel<7, 2, 1>"],  # the fused decode writing only the lost slices
+    "recover": ["tec::dcls::dec_class_"],  # the recover class kernels (decode_class.hip), side by side
     "outer": ["tec::rs16k::rs16_matrix_kernel<9, 32, false>"],  # OuterCoder(17, 50) encode: 17 x 33 matrix
     "outer_decode": ["tec::rs16k::rs16_matrix_kernel<5, 32, true>"],  # 17 restored from 17 (3 launches per step)
 }
@@ -168,9 +168,10 @@ LAUNCHES_PER_STEP = {"outer_decode": 3}
 
 
 def kernel_names(mode: str, decode_jit: str = "async", pattern: str = "worst") -> list:
-    # random survivor sets serve ~1 object per pattern: no pattern reaches a compiled kernel
+    # random survivor sets serve ~1 object per pattern: no pattern reaches a hipRTC kernel, every
+    # stripe runs its class's kernel (decode_class.hip)
     if mode == "decode" and (decode_jit == "off" or pattern == "random"):
-        return ["tec::dstage::dec_stage_kernel<7, 2, 1>"]
+        return ["tec::dcls::dec_class_"]
     return KERNELS.get(mode, [])
 
 

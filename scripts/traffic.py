@@ -35,7 +35,8 @@ def per_step(d, m):
             kn = next((n for n in names if k.startswith(n) or ("void " + n) in k), None)
             if kn is None:
                 continue
-            key = (kn, r["Counter_Name"])
+            # per distinct kernel (each decode / recover class kernel is launched once per step)
+            key = (k, r["Counter_Name"])
             disp = per.setdefault(key, {})
             disp[r.get("Dispatch_Id", "")] = disp.get(r.get("Dispatch_Id", ""), 0.0) + float(r["Counter_Value"])
         for (kn, c), disp in per.items():

@@ -103,6 +103,7 @@ struct CTile {
     // one decoded word to data chunk offset `ob` at plane offset `po`, where it was loaded; a
     // word across the end of the stripe's output share is written byte by byte
     __device__ __forceinline__ void out_st(u32 ob, u32 po, u32 v) const {
+        if (ob == kDropBase) return;  // uniform: a column-0 parity node's row is not output
         const u32 o = ob + po + vcol;
         if (full) {  // uniform: every data row of the stripe lies inside its output share
             __builtin_amdgcn_raw_buffer_store_b32(v, rs_out, (int)o, 0, 2);

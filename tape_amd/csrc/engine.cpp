@@ -1545,7 +1545,11 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     size_t call_stripes = 0;
     for (auto &o : offs) call_stripes += groups[o.first].size();
     for (const ClassGrp &cg : cls) call_stripes += cg.jobs.size();
-    const uint32_t class_g = call_stripes <= dec_small_max ? 1u : 2u;
+    static const uint32_t class_g_big = [] {  // measurement option TEC_DEC_CLASS_G (1 or 2)
+        const char *e = tec_knob("TEC_DEC_CLASS_G");
+        return e && atoi(e) == 1 ? 1u : 2u;
+    }();
+    const uint32_t class_g = call_stripes <= dec_small_max ? 1u : class_g_big;
     const bool small_dec = call_stripes <= dec_small_max;
     auto dec_args = [&](const std::pair<uint64_t, size_t> &o) {
         const uint64_t cs = o.first >> 32;
