@@ -1335,7 +1335,16 @@ def percall_bench(args, torch, dist, world, rank, dev):
                 for _ in range(reps):
                     fn()
                 ms = (time.perf_counter() - t) / reps * 1e3
-                row[name] = {"ms_per_call": round(ms, 3), "object_GiBps": round(L / (ms / 1e3) / 2**30, 3)}
+                # the calls' device time alone (HIP events around each call's kernels), in a
+                # second pass so the events do not touch the timed one
+                batch.kernel_time_ms()
+                batch.kernel_timing(True)
+                for _ in range(reps):
+                    fn()
+                batch.kernel_timing(False)
+                kms, kn = batch.kernel_time_ms()
+                row[name] = {"ms_per_call": round(ms, 3), "object_GiBps": round(L / (ms / 1e3) / 2**30, 3),
+                             "kernel_ms_per_call": round(kms / max(1, reps), 3)}
             ok = ok and np.array_equal(dec, src) and np.array_equal(rep, out[:sl])
             res[f"{L >> 20}MiB_{kind}"] = row
         if rank == 0 and args.cpu_sample > 0:
