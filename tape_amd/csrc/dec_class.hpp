@@ -39,6 +39,7 @@ namespace tec {
 // first among its column's erased nodes (dec_class_lost_first, with the matrix rows), and the
 // representative's lost node is the first erased node of column yL.
 constexpr int kDecClassN = 20, kDecClassK = 7, kDecClassesDecode = 8, kDecClasses = 24;
+constexpr int kDecClassSplit = 4;  // per-call kernel: waves sharing one 64-column group
 constexpr uint64_t kDecClassOutMask = 0x3ffull;  // decode: every column-0 node is an output
 
 struct DecClassSpec {
@@ -122,8 +123,12 @@ inline bool dec_class_prog(const ClayHost &h, int id, GpePattern &P, DecProgHdr 
     return found;
 }
 
-// LDS bytes of a class kernel with G waves per workgroup (lane-private slot rows, 4 B per lane).
-inline size_t dec_class_lds(uint32_t nslots, int G) { return (size_t)(nslots ? nslots : 1) * G * 64u * 4u; }
+// LDS bytes of a class kernel: the batch kernel (G = 2) holds its lane-private slot rows, the
+// per-call kernel (G = 1, kDecClassSplit waves on one 64-column group) every slot and scratch row.
+inline size_t dec_class_lds(uint32_t nslots, uint32_t nscratch, uint32_t nring, int G) {
+    const uint32_t rows = G == 1 ? 2 * nring + nslots + nscratch : nslots;
+    return (size_t)(rows ? rows : 1) * G * 64u * 4u;
+}
 
 // Kernel source of class `id` (one translation unit; decode_class_dev.hpp has the helpers).
 // t_u: the type-1 coefficient (C = t_u (U ^ Cp) ^ Cp).
@@ -132,6 +137,7 @@ inline size_t dec_class_lds(uint32_t nslots, int G) { return (size_t)(nslots ? n
 // its products instead of at its start.
 struct DecClassGenOpt {
     int wpe = 4;
+    int deep = 4;  // the per-call kernel's input-load lead, in steps
     bool late = false;
     bool tab4 = true;  // 2-bit-field product tables (PermTab4); false: the 3/3/2-bit PermTab
 };
@@ -167,9 +173,36 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
          "%u scratch rows\n", id, cs.a0, cs.yl < 0 ? "decode" : cs.yl == 0 ? "recover, lost node in column 0" :
          "recover, lost node in column 1", NS, H.nslots, H.nscratch);
     s += "#include \"decode_class_dev.hpp\"\nnamespace tec {\nnamespace dcls {\n";
-    emit("template <int G>\n__global__ void __attribute__((amdgpu_flat_work_group_size(1, G * 64), amdgpu_waves_per_eu(%d)))\n"
-         "dec_class_%d(DecClassArgs a) {\n", opt.wpe, id);
-    s += "  extern __shared__ __attribute__((aligned(16))) u32 lds[];\n  CTile<G> T(a, reinterpret_cast<u8 *>(lds));\n";
+    // One body, two kernels: the batch kernel (G = 2 waves per workgroup, the register budget of
+    // opt.wpe waves per SIMD, each step's input loads issued one step ahead) and the per-call
+    // kernel (one wave per workgroup, few waves on the chip, so registers are free: the input
+    // loads -- read-only slices, never written by the kernel -- issued `deep` steps ahead, which
+    // takes the global-memory latency off a lone wave's 100-step chain).  Scratch loads keep
+    // their place after the previous step's stores.
+    // the per-call kernel's input ring: per step, its own rows, input partners and type-1
+    // partners, in that order (ring row i of the step's slot)
+    uint32_t nring = 1;
+    for (const DecStep &S : steps) {
+        uint32_t c = (uint32_t)NK;
+        for (int j = 0; j < NK; j++) c += S.kk[j] == kKnInput;
+        for (int e = 0; e < NE; e++) c += S.ek[e] == kErType1;
+        nring = std::max(nring, c);
+    }
+    auto body = [&](bool small) {
+    const int depth = small ? opt.deep : 1, W = small ? kDecClassSplit : 1;
+    // the per-call kernel: W compute waves share one 64-column group and a loader wave (wv == W)
+    // brings each step's input rows into a two-slot LDS ring a step ahead, issuing its global
+    // loads `depth` steps ahead (gfx9 counts loads and stores on one vmcnt, so compute waves that
+    // loaded would wait on their own output stores every step); every parked value lives in LDS,
+    // shared by the waves: ring rows first, then slots, then scratch rows
+    const uint32_t ring0 = 0, slot0 = small ? 2 * nring : 0u, scr0 = small ? 2 * nring + H.nslots : 0u;
+    if (small)
+        emit("__global__ void __attribute__((amdgpu_flat_work_group_size(1, %d), amdgpu_waves_per_eu(1)))\n"
+             "dec_class_%d_small(DecClassArgs a) {\n  constexpr int G = 1;\n", 64 * (W + 1), id);
+    else
+        emit("__global__ void __attribute__((amdgpu_flat_work_group_size(1, 128), amdgpu_waves_per_eu(%d)))\n"
+             "dec_class_%d(DecClassArgs a) {\n  constexpr int G = 2;\n", opt.wpe, id);
+    emit("  extern __shared__ __attribute__((aligned(16))) u32 lds[];\n  CTile<G, %d> T(a, reinterpret_cast<u8 *>(lds));\n", W);
     // per-workgroup offsets: known slices, plane digits, data chunks (only what the program uses;
     // the rest is dead code)
     for (int j = 0; j < NK; j++) emit("  const u32 kb%d = T.kbase(T.K(%d));\n", j, j);
@@ -184,8 +217,31 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
     auto poff = [&](uint32_t z) {
         return "pz0_" + std::to_string(z / 10) + " + pz1_" + std::to_string(z % 10);
     };
-    auto loads = [&](int st) {
+    // per-call kernel: the step's input rows in ring order (expression of the global load)
+    auto ring_list = [&](int st) {
+        std::vector<std::string> L;
+        const DecStep &S = steps[st];
+        for (int j = 0; j < NK; j++) L.push_back("T.ld_own(kb" + std::to_string(j) + ", " + poff(S.z) + ")");
+        for (int j = 0; j < NK; j++)
+            if (S.kk[j] == kKnInput) L.push_back("T.ld(kb" + std::to_string(kidx((int)(S.kp[j] & 0xffu))) + ", " + poff(S.kp[j] >> 8) + ")");
+        for (int e = 0; e < NE; e++)
+            if (S.ek[e] == kErType1) L.push_back("T.ld(kb" + std::to_string(kidx((int)(S.ep[e] & 0xffu))) + ", " + poff(S.ep[e] >> 8) + ")");
+        return L;
+    };
+    auto ring_row = [&](int st, int i) { return ring0 + (uint32_t)(st & 1) * nring + (uint32_t)i; };
+    // loader: issue step st's global loads into L<st>_i (declared at function scope)
+    auto loader_issue = [&](int st) {
         if (st >= NS) return;
+        const auto L = ring_list(st);
+        for (size_t i = 0; i < L.size(); i++) emit("  L%d_%zu = %s;\n", st, i, L[i].c_str());
+    };
+    auto loader_put = [&](int st) {  // loader: step st's rows into its ring slot
+        if (st >= NS) return;
+        const auto L = ring_list(st);
+        for (size_t i = 0; i < L.size(); i++) emit("  T.lds_st(%u, L%d_%zu);\n", ring_row(st, (int)i), st, i);
+    };
+    auto loads = [&](int st) {
+        if (st >= NS || small) return;
         const DecStep &S = steps[st];
         for (int j = 0; j < NK; j++) {
             emit("  const u32 o%s = T.ld_own(kb%d, %s);\n", id2(st, j).c_str(), j, poff(S.z).c_str());
@@ -201,13 +257,26 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
     auto scr_loads = [&](int st) {
         if (st >= NS) return;
         const DecStep &S = steps[st];
+        if (small) return;  // LDS rows: read where they are used
         for (int j = 0; j < NK; j++)
             if (S.kk[j] == kKnLoc && lty(S.kp[j]) == kLocScratch) emit("  const u32 q%s = T.scr_ld(%u);\n", id2(st, j).c_str(), lix(S.kp[j]));
         for (int e = 0; e < NE; e++)
             if (S.ek[e] == kErFinish && lty(S.ep[e]) == kLocScratch) emit("  const u32 r%s = T.scr_ld(%u);\n", id2(st, e).c_str(), lix(S.ep[e]));
     };
-    loads(0);
+    // a location's LDS row (per-call kernel: scratch rows after the slots)
+    auto lrow = [&](uint32_t loc) { return lty(loc) == kLocSlot ? slot0 + lix(loc) : scr0 + lix(loc); };
+    for (int d = 0; d < depth; d++) loads(d);
     scr_loads(0);
+    if (small) {  // the loader's registers, its first `depth` steps of loads, step 0's ring slot
+        for (int st = 0; st < NS; st++) {
+            const size_t nl = ring_list(st).size();
+            for (size_t i = 0; i < nl; i++) emit("  u32 L%d_%zu;\n", st, i);
+        }
+        emit("  if (T.wv == %du) {\n", W);
+        for (int d = 0; d < depth; d++) loader_issue(d);
+        loader_put(0);
+        s += "  }\n  T.sync();\n";
+    }
     for (int st = 0; st < NS; st++) {
         const DecStep &S = steps[st];
         auto put = [&](uint32_t loc, const std::string &v) {
@@ -215,39 +284,71 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
             if (lty(loc) == kLocStage) {
                 const uint32_t it = S.out[lix(loc)];
                 emit("  T.out_st(ob%u, %s, %s);\n", it & 0xffu, poff((it >> 8) & 0xffu).c_str(), v.c_str());
-            } else if (lty(loc) == kLocSlot) {
-                emit("  T.lds_st(%u, %s);\n", lix(loc), v.c_str());
+            } else if (lty(loc) == kLocSlot || small) {
+                emit("  T.lds_st(%u, %s);\n", lrow(loc), v.c_str());
             } else {
                 emit("  T.scr_st(%u, %s);\n", lix(loc), v.c_str());
             }
         };
+        // per-call kernel: which of the W waves does a known row's copy / an erased row's work
+        std::vector<int> own_e(NE, 0);
+        int nw = 0;
+        for (int e = 0; e < NE; e++)
+            if (S.ek[e] != kErSkip) own_e[e] = nw++ % W;
         emit("  // step %d: plane (%u, %u)\n", st, S.z / 10, S.z % 10);
-        if (!opt.late) loads(st + 1);
+        if (!opt.late) loads(st + depth);
+        if (small) {
+            // this step's input rows from the ring (compute waves; the loader's copy is unused)
+            const DecStep &S0 = S;
+            int i = 0;
+            for (int j = 0; j < NK; j++) emit("  const u32 o%s = T.lds_ld(%u);\n", id2(st, j).c_str(), ring_row(st, i++));
+            for (int j = 0; j < NK; j++)
+                if (S0.kk[j] == kKnInput) emit("  const u32 p%s = T.lds_ld(%u);\n", id2(st, j).c_str(), ring_row(st, i++));
+            for (int e = 0; e < NE; e++)
+                if (S0.ek[e] == kErType1) emit("  const u32 t%s = T.lds_ld(%u);\n", id2(st, e).c_str(), ring_row(st, i++));
+            // loader: step st + depth's global loads, step st + 1's rows into the other slot
+            emit("  if (T.wv == %du) {\n", W);
+            loader_issue(st + depth);
+            loader_put(st + 1);
+            s += "  }\n";
+        }
         // uncouple the known nodes (known data rows are copied out as they are)
         for (int j = 0; j < NK; j++) {
             const std::string id = id2(st, j);
             const char *i = id.c_str();
             if (S.kk[j] == kKnRed) emit("  const u32 u%s = o%s;\n", i, i);
             else if (S.kk[j] == kKnInput) emit("  const u32 u%s = pft3(o%s, p%s);\n", i, i, i);
-            else if (lty(S.kp[j]) == kLocSlot) emit("  const u32 u%s = pft3(o%s, T.lds_ld(%u));\n", i, i, lix(S.kp[j]));
+            else if (lty(S.kp[j]) == kLocSlot || small) emit("  const u32 u%s = pft3(o%s, T.lds_ld(%u));\n", i, i, lrow(S.kp[j]));
             else emit("  const u32 u%s = pft3(o%s, q%s);\n", i, i, i);
-            put(S.kout[j], "o" + id);
+            if (!small) put(S.kout[j], "o" + id);
         }
         // pair partners' U, read before this step's writes
         for (int e = 0; e < NE; e++) {
             if (S.ek[e] != kErFinish) continue;
             const std::string id = id2(st, e);
-            if (lty(S.ep[e]) == kLocSlot) emit("  const u32 v%s = T.lds_ld(%u);\n", id.c_str(), lix(S.ep[e]));
+            if (lty(S.ep[e]) == kLocSlot || small) emit("  const u32 v%s = T.lds_ld(%u);\n", id.c_str(), lrow(S.ep[e]));
             else emit("  const u32 v%s = r%s;\n", id.c_str(), id.c_str());
+        }
+        if (small) {
+            // every wave has read what this step reads before any wave writes (a location is
+            // reused from its consumer step on); the known rows' copies, spread over the waves
+            s += "  T.sync();\n";
+            for (int j = 0; j < NK; j++)
+                if (S.kout[j] != kLocNone) {
+                    emit("  if (T.wv == %du) {\n", j % W);
+                    put(S.kout[j], "o" + id2(st, j));
+                    s += "  }\n";
+                }
         }
         // MDS: the erased U's this step needs, v_perm products against the pattern's matrix
         bool any = false;
         for (int e = 0; e < NE; e++) any = any || S.ek[e] != kErSkip;
-        if (any) {
+        for (int w = 0; w < (any ? W : 0); w++) {
+            if (small) emit("  if (T.wv == %du) {\n", w);
             for (int j = 0; j < NK; j++)
                 emit("  const %s s%s(u%s);\n", opt.tab4 ? "Sel4" : "Sel", id2(st, j).c_str(), id2(st, j).c_str());
             for (int e = 0; e < NE; e++) {
-                if (S.ek[e] == kErSkip) continue;
+                if (S.ek[e] == kErSkip || own_e[e] != w) continue;
                 const std::string a = "a" + id2(st, e);
                 emit("  u32 %s = 0u;\n  { const auto D = T.%s();\n", a.c_str(), opt.tab4 ? "mat4" : "mat");
                 for (int j = 0; j + 1 < NK; j += 2)
@@ -281,15 +382,19 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
                     default: break;
                 }
             }
+            if (small) s += "  }\n";
         }
-        if (opt.late) loads(st + 1);
+        if (small) s += "  T.sync();\n";  // this step's values visible to every wave
+        if (opt.late) loads(st + depth);
         scr_loads(st + 1);
     }
     s += "}\n";
-    emit("template __global__ void dec_class_%d<1>(DecClassArgs);\ntemplate __global__ void dec_class_%d<2>(DecClassArgs);\n", id, id);
-    emit("void dec_class_reg_%d(DecClassEntry &e) {\n  e.fn[0] = reinterpret_cast<const void *>(&dec_class_%d<1>);\n"
-         "  e.fn[1] = reinterpret_cast<const void *>(&dec_class_%d<2>);\n  e.nslots = %uu;\n  e.nscratch = %uu;\n}\n",
-         id, id, id, H.nslots, H.nscratch);
+    };
+    body(true);
+    body(false);
+    emit("void dec_class_reg_%d(DecClassEntry &e) {\n  e.fn[0] = reinterpret_cast<const void *>(&dec_class_%d_small);\n"
+         "  e.fn[1] = reinterpret_cast<const void *>(&dec_class_%d);\n  e.nslots = %uu;\n  e.nscratch = %uu;\n"
+         "  e.nring = %uu;\n}\n", id, id, id, H.nslots, H.nscratch, nring);
     s += "}  // namespace dcls\n}  // namespace tec\n";
     return s;
 }

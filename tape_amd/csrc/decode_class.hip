@@ -34,7 +34,7 @@ uint32_t dec_class_wgs(uint32_t sc, uint32_t G) {
 
 size_t dec_class_scratch_bytes(int id, uint32_t njobs, uint32_t sc, uint32_t G) {
     uint32_t ns = 0, nscr = 0;
-    if (!dec_class_info(id, &ns, &nscr)) return 0;
+    if (!dec_class_info(id, &ns, &nscr) || G == 1) return 0;  // the per-call kernel parks in LDS
     return (size_t)njobs * dec_class_wgs(sc, G) * (nscr ? nscr : 1) * G * 256u;
 }
 
@@ -63,12 +63,14 @@ hipError_t launch_dec_class(int id, const GpeJob *jobs, const GpePattern *patter
     a.out_full = full > 0xffffffffull ? 0xffffffffu : (uint32_t)full;
     const uint64_t blocks = (uint64_t)njobs * a.wgs_per_stripe;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    const size_t lds = dec_class_lds(nslots, (int)G);
+    const size_t lds = dec_class_lds(nslots, nscr, dec_class_table()[id].nring, (int)G);
     const void *fn = dec_class_table()[id].fn[G - 1];
     hipError_t e = ensure_dyn_lds(fn, lds);
     if (e != hipSuccess) return e;
     void *args[] = {&a};
-    e = hipLaunchKernel(fn, dim3((uint32_t)blocks), dim3(G * 64), args, lds, s);
+    // G = 1: the per-call kernel, kDecClassSplit compute waves and a loader wave per 64-column group
+    const uint32_t threads = G == 1 ? 64u * (kDecClassSplit + 1) : G * 64u;
+    e = hipLaunchKernel(fn, dim3((uint32_t)blocks), dim3(threads), args, lds, s);
     return e != hipSuccess ? e : hipGetLastError();
 }
 

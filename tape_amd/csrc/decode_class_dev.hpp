@@ -32,26 +32,30 @@ struct DecClassArgs {
 // host registry entry of one class (decode_class.hip)
 struct DecClassEntry {
     const void *fn[2] = {nullptr, nullptr};  // G = 1, 2
-    uint32_t nslots = 0, nscratch = 0;
+    uint32_t nslots = 0, nscratch = 0, nring = 0;  // nring: the per-call kernel's ring rows per step
 };
 
 __device__ __forceinline__ u32 pft3(u32 a, u32 b) { return a ^ xt(a ^ b); }  // 3a ^ 2b (PFT, A3)
 
-template <int G>
+// G waves of columns per workgroup (one 4-byte word per lane); W waves share those columns and
+// split each step's work (the per-call kernel: W = 4, all values in LDS, a barrier per step)
+template <int G, int W = 1>
 struct CTile {
     typedef const __attribute__((address_space(4))) GpePattern cPat;
     typedef const __attribute__((address_space(4))) PermTab cTab;
     static constexpr u32 RS = G * 256u;  // LDS / scratch row stride (G waves x 64 lanes x 4 B)
     u8 *lds8;
     cPat *pat;
-    u32 lane, col_local, vcol, sc, olen, rot, n, in_stride, out_stride;
+    u32 lane, col_local, vcol, sc, olen, rot, n, in_stride, out_stride, wv;
     bool full;
     __amdgpu_buffer_rsrc_t rs_in, rs_out, rs_scr;
 
     __device__ __forceinline__ CTile(const DecClassArgs &a, u8 *lds) {
         lds8 = lds;
         lane = threadIdx.x & 63u;
-        col_local = threadIdx.x * 4u;
+        const u32 t = threadIdx.x % (G * 64u);  // this thread's column word within the workgroup's
+        wv = __builtin_amdgcn_readfirstlane(threadIdx.x / (G * 64u));  // which of the W sharing waves
+        col_local = t * 4u;
         const u32 tile = xcd_tile(blockIdx.x, gridDim.x);
         const u32 job = tile / a.wgs_per_stripe, seg = tile - job * a.wgs_per_stripe;
         typedef const __attribute__((address_space(4))) GpeJob cJob;
@@ -62,7 +66,7 @@ struct CTile {
         rot = J.rot;
         in_stride = (u32)a.in_stride;
         out_stride = (u32)a.out_stride;
-        u32 w = seg * G * 64u + threadIdx.x;
+        u32 w = seg * G * 64u + t;
         if (w >= a.wps) w = a.wps - 1;  // words past the stripe alias the last (same values, same bytes)
         const u32 col = w * 4u;
         vcol = col + 4u > a.sc ? a.sc - 4u : col;  // the row's last 4 bytes for a word past the sub-chunk
@@ -73,6 +77,8 @@ struct CTile {
         const u32 nscr = a.nscratch ? a.nscratch : 1u;
         rs_scr = __builtin_amdgcn_make_buffer_rsrc(a.scratch + (u64)tile * nscr * RS, 0, (int)(nscr * RS), 0x00020000);
     }
+    // the W sharing waves' LDS hand-off between steps (LDS only: loads in flight keep flying)
+    __device__ __forceinline__ void sync() const { lds_barrier(); }
     // the pattern's known / erased node ids (ascending), scalar loads
     __device__ __forceinline__ u32 K(int i) const { return pat->known[i]; }
     __device__ __forceinline__ u32 E(int i) const { return pat->erased[i]; }
@@ -117,19 +123,17 @@ struct CTile {
     // The matrix of one erased row: the pattern pointer is laundered each time so the row's table
     // loads are issued where they are used, not hoisted over the straight-line program (the
     // 13 x 7 tables of 5 dwords are 455 SGPRs: hoisted, they spill).
-    __device__ __forceinline__ cTab (*mat())[kGpeMaxKnown] {
+    __device__ __forceinline__ cTab (*mat() const)[kGpeMaxKnown] {
         u64 p = (u64)(uintptr_t)pat;
         asm volatile("; mat" : "+s"(p));
-        pat = (cPat *)(uintptr_t)p;
-        return pat->D;
+        return ((cPat *)(uintptr_t)p)->D;
     }
     // the 2-bit-field tables of one erased row (laundered as mat())
     typedef const __attribute__((address_space(4))) u32 cU32;
-    __device__ __forceinline__ cU32 (*mat4())[kClsMaxK][4] {
+    __device__ __forceinline__ cU32 (*mat4() const)[kClsMaxK][4] {
         u64 p = (u64)(uintptr_t)pat;
-        asm volatile("; mat4" : "+s"(p));
-        pat = (cPat *)(uintptr_t)p;
-        return pat->D4;
+        asm volatile("; mat4" : "+s"(p));  // a fresh value per call: the loads are not hoisted
+        return ((cPat *)(uintptr_t)p)->D4;
     }
     __device__ __forceinline__ static u32 mul2(u32 acc, cU32 (*D)[kClsMaxK][4], int e, int j, const Sel4 &x, const Sel4 &y) {
         cU32 *p = D[e][j], *q = D[e][j + 1];

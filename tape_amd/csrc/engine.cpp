@@ -1257,6 +1257,9 @@ bool dec_store_slots(te_clay *c, const std::vector<const te_clay::DecCache *> &c
     return true;
 }
 
+// A decode call of at most this many stripes is a per-call decode: one wave per workgroup.
+constexpr size_t kDecSmallStripes = 64;
+
 // Items with lost >= 0 (node recover) need the staged kernel: TE_ERR_UNSUPPORTED, before anything
 // is enqueued, when a pattern has no plane program (the caller then decodes and re-encodes).
 int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices, const DecItem *items,
@@ -1445,9 +1448,12 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         // with more class groups than streams some launches would run after others, so such a
         // call runs on the table-driven kernel in one launch (per call 64 MiB: 3.67 ms as
         // classes against 3.00, r06)
-        size_t ncls = 0;
+        // (per-call decodes of <= 64 stripes run the classes' one-wave kernels, whose input loads
+        // lead by four steps: their chains are short enough to run a few one after another)
+        size_t ncls = 0, nall = 0;
         for (const ClassGrp &cg : cls) ncls += cg.jobs.size();
-        if (cls.size() > (size_t)class_streams && ncls < 1024) {
+        for (auto &kv : groups) nall += kv.second.size();
+        if (cls.size() > (size_t)class_streams && ncls < 1024 && ncls + nall > kDecSmallStripes) {
             for (ClassGrp &cg : cls) groups[cg.key].insert(groups[cg.key].end(), cg.jobs.begin(), cg.jobs.end());
             cls.clear();
         }
@@ -1540,7 +1546,7 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     // step.  Measurement option TEC_DEBUG_KNOBS=1 TEC_DEC_SMALL=n: the stripe bound (0: never).
     static const size_t dec_small_max = [] {
         const char *e = tec_knob("TEC_DEC_SMALL");
-        return e ? (size_t)atoi(e) : (size_t)64;
+        return e ? (size_t)atoi(e) : kDecSmallStripes;
     }();
     size_t call_stripes = 0;
     for (auto &o : offs) call_stripes += groups[o.first].size();
@@ -3513,12 +3519,33 @@ int te_slicer_decode(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *const 
     r = ensure_stream(c);
     if (r) return r;
     const size_t total = (size_t)h.n * slice_len;
+    it.in_base = 0;
+    it.out_off = 0;
+    // A per-call decode (<= 64 stripes, the one-wave class kernels) reads its slices from page-
+    // locked host staging and writes the object to page-locked memory over PCIe, with no H2D /
+    // D2H copy around a 0.3 ms kernel whose loader wave issues its loads four steps ahead; the
+    // slices are gathered into the staging by the copy pool (the repair call's scheme).
+    // Measurement option TEC_DEBUG_KNOBS=1 TEC_DECODE_ZC=0: the copies instead.
+    static const bool zc = [] { const char *e = tec_knob("TEC_DECODE_ZC"); return !(e && e[0] == '0'); }();
+    if (zc && it.ns <= kDecSmallStripes) {
+        TE_HIP(c->hio_in.ensure(total));
+        std::vector<tec::CopyPool::Seg> segs;
+        for (int i = 0; i < h.n; i++)
+            if (slices[i]) segs.push_back({c->hio_in.u8() + (size_t)i * slice_len, slices[i], slice_len});
+        copy_pool(c->device).run(segs);
+        const bool out_pinned = host_pinned(out);
+        if (!out_pinned) TE_HIP(c->hio_out.ensure(it.blob_len));
+        uint8_t *dst = out_pinned ? out : c->hio_out.u8();
+        r = decode_enqueue(c, cfg, c->hio_in.u8(), &it, 1, dst, c->stream, false);
+        if (r) return r;
+        TE_HIP(hipStreamSynchronize(c->stream));
+        if (!out_pinned) copy_pool(c->device).run({{out, c->hio_out.p, it.blob_len}});
+        return TE_OK;
+    }
     TE_HIP(c->io_in.ensure(total));
     TE_HIP(c->io_out.ensure(it.blob_len));
     r = upload_slices(c, slices, slice_len);
     if (r) return r;
-    it.in_base = 0;
-    it.out_off = 0;
     r = decode_enqueue(c, cfg, c->io_in.as<uint8_t>(), &it, 1, c->io_out.as<uint8_t>(), c->stream, false);
     if (r) return r;
     TE_HIP(hipMemcpyAsync(out, c->io_out.p, it.blob_len, hipMemcpyDeviceToHost, c->stream));
