@@ -3483,13 +3483,30 @@ int te_clay_decode(te_clay *c, const uint8_t *const *chunks, size_t cs, uint8_t 
     int r = ensure_stream(c);
     if (r) return r;
     const size_t total = (size_t)h.n * cs;
+    DecItem it{};
+    it.in_base = 0; it.slice_len = cs; it.blob_len = (uint64_t)h.k * cs; it.stripe = it.blob_len; it.ns = 1; it.cs = cs;
+    it.out_off = 0; it.avail = avail;
+    // one stripe: the zero-copy per-call path of te_slicer_decode (staging read and written over PCIe)
+    static const bool zc = [] { const char *e = tec_knob("TEC_DECODE_ZC"); return !(e && e[0] == '0'); }();
+    if (zc) {
+        TE_HIP(c->hio_in.ensure(total));
+        std::vector<tec::CopyPool::Seg> segs;
+        for (int i = 0; i < h.n; i++)
+            if (chunks[i]) segs.push_back({c->hio_in.u8() + (size_t)i * cs, chunks[i], cs});
+        copy_pool(c->device).run(segs);
+        const bool out_pinned = host_pinned(out);
+        if (!out_pinned) TE_HIP(c->hio_out.ensure((size_t)h.k * cs));
+        uint8_t *dst = out_pinned ? out : c->hio_out.u8();
+        r = decode_enqueue(c, nullptr, c->hio_in.u8(), &it, 1, dst, c->stream, true);
+        if (r) return r;
+        TE_HIP(hipStreamSynchronize(c->stream));
+        if (!out_pinned) copy_pool(c->device).run({{out, c->hio_out.p, (size_t)h.k * cs}});
+        return TE_OK;
+    }
     TE_HIP(c->io_in.ensure(total));
     TE_HIP(c->io_out.ensure((size_t)h.k * cs));
     r = upload_slices(c, chunks, cs);
     if (r) return r;
-    DecItem it{};
-    it.in_base = 0; it.slice_len = cs; it.blob_len = (uint64_t)h.k * cs; it.stripe = it.blob_len; it.ns = 1; it.cs = cs;
-    it.out_off = 0; it.avail = avail;
     r = decode_enqueue(c, nullptr, c->io_in.as<uint8_t>(), &it, 1, c->io_out.as<uint8_t>(), c->stream, true);
     if (r) return r;
     TE_HIP(hipMemcpyAsync(out, c->io_out.p, (size_t)h.k * cs, hipMemcpyDeviceToHost, c->stream));
