@@ -140,6 +140,8 @@ struct DecClassGenOpt {
     int deep = 4;  // the per-call kernel's input-load lead, in steps
     bool late = false;
     bool tab4 = true;  // 2-bit-field product tables (PermTab4); false: the 3/3/2-bit PermTab
+    int own_aux = 2;   // cache policy of the batch kernel's own-row loads (2: non-temporal)
+    int scr_aux = 0;   // ... and of its scratch loads (each scratch row is read once)
 };
 
 inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecProgHdr &Hout,
@@ -244,7 +246,7 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
         if (st >= NS || small) return;
         const DecStep &S = steps[st];
         for (int j = 0; j < NK; j++) {
-            emit("  const u32 o%s = T.ld_own(kb%d, %s);\n", id2(st, j).c_str(), j, poff(S.z).c_str());
+            emit("  const u32 o%s = T.ld_aux<%d>(kb%d, %s);\n", id2(st, j).c_str(), opt.own_aux, j, poff(S.z).c_str());
             if (S.kk[j] == kKnInput)
                 emit("  const u32 p%s = T.ld(kb%d, %s);\n", id2(st, j).c_str(), kidx((int)(S.kp[j] & 0xffu)),
                      poff(S.kp[j] >> 8).c_str());
@@ -259,9 +261,9 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
         const DecStep &S = steps[st];
         if (small) return;  // LDS rows: read where they are used
         for (int j = 0; j < NK; j++)
-            if (S.kk[j] == kKnLoc && lty(S.kp[j]) == kLocScratch) emit("  const u32 q%s = T.scr_ld(%u);\n", id2(st, j).c_str(), lix(S.kp[j]));
+            if (S.kk[j] == kKnLoc && lty(S.kp[j]) == kLocScratch) emit("  const u32 q%s = T.scr_ld<%d>(%u);\n", id2(st, j).c_str(), opt.scr_aux, lix(S.kp[j]));
         for (int e = 0; e < NE; e++)
-            if (S.ek[e] == kErFinish && lty(S.ep[e]) == kLocScratch) emit("  const u32 r%s = T.scr_ld(%u);\n", id2(st, e).c_str(), lix(S.ep[e]));
+            if (S.ek[e] == kErFinish && lty(S.ep[e]) == kLocScratch) emit("  const u32 r%s = T.scr_ld<%d>(%u);\n", id2(st, e).c_str(), opt.scr_aux, lix(S.ep[e]));
     };
     // a location's LDS row (per-call kernel: scratch rows after the slots)
     auto lrow = [&](uint32_t loc) { return lty(loc) == kLocSlot ? slot0 + lix(loc) : scr0 + lix(loc); };

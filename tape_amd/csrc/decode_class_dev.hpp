@@ -94,10 +94,15 @@ struct CTile {
     __device__ __forceinline__ u32 ld(u32 base, u32 off) const {
         return __builtin_amdgcn_raw_buffer_load_b32(rs_in, (int)vcol, (int)(base + off), 0);
     }
+    template <int AUX>
+    __device__ __forceinline__ u32 ld_aux(u32 base, u32 off) const {
+        return __builtin_amdgcn_raw_buffer_load_b32(rs_in, (int)vcol, (int)(base + off), AUX);
+    }
     __device__ __forceinline__ u32 lds_ld(u32 row) const { return *reinterpret_cast<const u32 *>(lds8 + row * RS + col_local); }
     __device__ __forceinline__ void lds_st(u32 row, u32 v) const { *reinterpret_cast<u32 *>(lds8 + row * RS + col_local) = v; }
+    template <int AUX = 0>
     __device__ __forceinline__ u32 scr_ld(u32 row) const {
-        return __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)col_local, (int)(row * RS), 0);
+        return __builtin_amdgcn_raw_buffer_load_b32(rs_scr, (int)col_local, (int)(row * RS), AUX);
     }
     __device__ __forceinline__ void scr_st(u32 row, u32 v) const {
         __builtin_amdgcn_raw_buffer_store_b32(v, rs_scr, (int)col_local, (int)(row * RS), 0);
