@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/.."
 name=$1; envs=$2
-d=varlib/gen_$name
+d=/tmp/varlib_gen_$name
 mkdir -p $d
 env $envs tape_amd/build/gen_dec_class $d
 ls $d/dec_class_[0-9]*.hip | xargs -P 8 -I{} /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC -Wno-unused-variable -Itape_amd/csrc -c -o {}.o {}

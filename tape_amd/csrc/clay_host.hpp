@@ -472,4 +472,37 @@ struct ClayHost {
     }
 };
 
+// (dec_prog programs of the generated class kernels and the hipRTC pattern kernels)
+// A type-1 step (erased N at plane z, known partner M at plane z') has both of the values the
+// partner's own step z' combines -- Cp = M's row at z' (its type-1 read) and C = N's new value --
+// so it parks M's U = pft3(Cp, C) in C's location and, when M is an output, stores Cp out itself
+// (epd: an item of its own step).  The partner's step then reads U (kKnPark) and does not load its
+// own row: the row was read once instead of twice.  Returns the number of fused pairs.
+inline int dec_prog_fuse_type1(const GpePattern &P, std::vector<DecStep> &steps) {
+    std::vector<int> at(256, -1);
+    for (size_t st = 0; st < steps.size(); st++) at[steps[st].z & 0xffu] = (int)st;
+    int fused = 0;
+    for (DecStep &S : steps)
+        for (uint32_t e = 0; e < P.nerased; e++) {
+            if (S.ek[e] != kErType1 || S.ed0[e] == kLocNone) continue;
+            const uint32_t M = S.ep[e] & 0xffu, zp = S.ep[e] >> 8;
+            if (zp >= 256 || at[zp] < 0) continue;
+            DecStep &T = steps[(size_t)at[zp]];
+            int j = -1;
+            for (uint32_t i = 0; i < P.nknown; i++)
+                if (P.known[i] == M) j = (int)i;
+            if (j < 0 || T.kk[j] != kKnLoc || T.kp[j] != S.ed0[e]) continue;
+            if (T.kout[j] != kLocNone) {  // M is an output: its row goes out from this step
+                if ((T.kout[j] >> 24) != kLocStage || S.nout >= (uint32_t)kDecMaxOutProg) continue;
+                S.out[S.nout] = T.out[T.kout[j] & 0xffffffu];
+                S.epd[e] = (kLocStage << 24) | S.nout++;
+                T.kout[j] = kLocNone;
+            }
+            S.ek[e] = kErType1U;
+            T.kk[j] = kKnPark;
+            fused++;
+        }
+    return fused;
+}
+
 }  // namespace tec

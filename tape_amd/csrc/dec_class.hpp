@@ -103,7 +103,8 @@ inline uint64_t dec_class_emask(const DecClassSpec &s) {
 
 // Program of class `id`'s representative: of the two row orientations the one with fewer
 // scratch rows (HBM traffic), then fewer MDS rows (VALU), within the LDS of two workgroups per CU.
-inline bool dec_class_prog(const ClayHost &h, int id, GpePattern &P, DecProgHdr &H, std::vector<DecStep> &steps) {
+inline bool dec_class_prog(const ClayHost &h, int id, GpePattern &P, DecProgHdr &H, std::vector<DecStep> &steps,
+                           bool fuse = true) {
     const DecClassSpec s = dec_class_spec(id);
     std::vector<uint16_t> pool;
     if (s.a0 < 0 || !h.gpe_pattern(dec_class_emask(s), P, pool)) return false;
@@ -120,6 +121,7 @@ inline bool dec_class_prog(const ClayHost &h, int id, GpePattern &P, DecProgHdr 
         const uint64_t cost = (H1.nslots + 2 > 53 ? 1ull << 40 : 0ull) + ((uint64_t)H1.nscratch << 20) + rows;
         if (!found || cost < best) { H = H1; steps.swap(st); best = cost; found = true; }
     }
+    if (found && fuse) dec_prog_fuse_type1(P, steps);
     return found;
 }
 
@@ -142,6 +144,7 @@ struct DecClassGenOpt {
     bool tab4 = true;  // 2-bit-field product tables (PermTab4); false: the 3/3/2-bit PermTab
     int own_aux = 2;   // cache policy of the batch kernel's own-row loads (2: non-temporal)
     int scr_aux = 0;   // ... and of its scratch loads (each scratch row is read once)
+    bool fuse = true;  // dec_class_fuse_type1
 };
 
 inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecProgHdr &Hout,
@@ -149,7 +152,7 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
     GpePattern P;
     DecProgHdr H;
     std::vector<DecStep> steps;
-    if (!dec_class_prog(h, id, P, H, steps)) return std::string();
+    if (!dec_class_prog(h, id, P, H, steps, opt.fuse)) return std::string();
     Hout = H;
     const DecClassSpec cs = dec_class_spec(id);
     const int NK = (int)P.nknown, NE = (int)P.nerased, NS = (int)steps.size();
@@ -185,9 +188,9 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
     // partners, in that order (ring row i of the step's slot)
     uint32_t nring = 1;
     for (const DecStep &S : steps) {
-        uint32_t c = (uint32_t)NK;
-        for (int j = 0; j < NK; j++) c += S.kk[j] == kKnInput;
-        for (int e = 0; e < NE; e++) c += S.ek[e] == kErType1;
+        uint32_t c = 0;
+        for (int j = 0; j < NK; j++) c += (S.kk[j] != kKnPark) + (S.kk[j] == kKnInput);
+        for (int e = 0; e < NE; e++) c += S.ek[e] == kErType1 || S.ek[e] == kErType1U;
         nring = std::max(nring, c);
     }
     auto body = [&](bool small) {
@@ -223,11 +226,12 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
     auto ring_list = [&](int st) {
         std::vector<std::string> L;
         const DecStep &S = steps[st];
-        for (int j = 0; j < NK; j++) L.push_back("T.ld_own(kb" + std::to_string(j) + ", " + poff(S.z) + ")");
+        for (int j = 0; j < NK; j++)
+            if (S.kk[j] != kKnPark) L.push_back("T.ld_own(kb" + std::to_string(j) + ", " + poff(S.z) + ")");
         for (int j = 0; j < NK; j++)
             if (S.kk[j] == kKnInput) L.push_back("T.ld(kb" + std::to_string(kidx((int)(S.kp[j] & 0xffu))) + ", " + poff(S.kp[j] >> 8) + ")");
         for (int e = 0; e < NE; e++)
-            if (S.ek[e] == kErType1) L.push_back("T.ld(kb" + std::to_string(kidx((int)(S.ep[e] & 0xffu))) + ", " + poff(S.ep[e] >> 8) + ")");
+            if (S.ek[e] == kErType1 || S.ek[e] == kErType1U) L.push_back("T.ld(kb" + std::to_string(kidx((int)(S.ep[e] & 0xffu))) + ", " + poff(S.ep[e] >> 8) + ")");
         return L;
     };
     auto ring_row = [&](int st, int i) { return ring0 + (uint32_t)(st & 1) * nring + (uint32_t)i; };
@@ -246,13 +250,14 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
         if (st >= NS || small) return;
         const DecStep &S = steps[st];
         for (int j = 0; j < NK; j++) {
-            emit("  const u32 o%s = T.ld_aux<%d>(kb%d, %s);\n", id2(st, j).c_str(), opt.own_aux, j, poff(S.z).c_str());
+            if (S.kk[j] != kKnPark)
+                emit("  const u32 o%s = T.ld_aux<%d>(kb%d, %s);\n", id2(st, j).c_str(), opt.own_aux, j, poff(S.z).c_str());
             if (S.kk[j] == kKnInput)
                 emit("  const u32 p%s = T.ld(kb%d, %s);\n", id2(st, j).c_str(), kidx((int)(S.kp[j] & 0xffu)),
                      poff(S.kp[j] >> 8).c_str());
         }
         for (int e = 0; e < NE; e++)
-            if (S.ek[e] == kErType1)
+            if (S.ek[e] == kErType1 || S.ek[e] == kErType1U)
                 emit("  const u32 t%s = T.ld(kb%d, %s);\n", id2(st, e).c_str(), kidx((int)(S.ep[e] & 0xffu)),
                      poff(S.ep[e] >> 8).c_str());
     };
@@ -261,7 +266,7 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
         const DecStep &S = steps[st];
         if (small) return;  // LDS rows: read where they are used
         for (int j = 0; j < NK; j++)
-            if (S.kk[j] == kKnLoc && lty(S.kp[j]) == kLocScratch) emit("  const u32 q%s = T.scr_ld<%d>(%u);\n", id2(st, j).c_str(), opt.scr_aux, lix(S.kp[j]));
+            if ((S.kk[j] == kKnLoc || S.kk[j] == kKnPark) && lty(S.kp[j]) == kLocScratch) emit("  const u32 q%s = T.scr_ld<%d>(%u);\n", id2(st, j).c_str(), opt.scr_aux, lix(S.kp[j]));
         for (int e = 0; e < NE; e++)
             if (S.ek[e] == kErFinish && lty(S.ep[e]) == kLocScratch) emit("  const u32 r%s = T.scr_ld<%d>(%u);\n", id2(st, e).c_str(), opt.scr_aux, lix(S.ep[e]));
     };
@@ -303,11 +308,12 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
             // this step's input rows from the ring (compute waves; the loader's copy is unused)
             const DecStep &S0 = S;
             int i = 0;
-            for (int j = 0; j < NK; j++) emit("  const u32 o%s = T.lds_ld(%u);\n", id2(st, j).c_str(), ring_row(st, i++));
+            for (int j = 0; j < NK; j++)
+                if (S0.kk[j] != kKnPark) emit("  const u32 o%s = T.lds_ld(%u);\n", id2(st, j).c_str(), ring_row(st, i++));
             for (int j = 0; j < NK; j++)
                 if (S0.kk[j] == kKnInput) emit("  const u32 p%s = T.lds_ld(%u);\n", id2(st, j).c_str(), ring_row(st, i++));
             for (int e = 0; e < NE; e++)
-                if (S0.ek[e] == kErType1) emit("  const u32 t%s = T.lds_ld(%u);\n", id2(st, e).c_str(), ring_row(st, i++));
+                if (S0.ek[e] == kErType1 || S0.ek[e] == kErType1U) emit("  const u32 t%s = T.lds_ld(%u);\n", id2(st, e).c_str(), ring_row(st, i++));
             // loader: step st + depth's global loads, step st + 1's rows into the other slot
             emit("  if (T.wv == %du) {\n", W);
             loader_issue(st + depth);
@@ -320,6 +326,8 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
             const char *i = id.c_str();
             if (S.kk[j] == kKnRed) emit("  const u32 u%s = o%s;\n", i, i);
             else if (S.kk[j] == kKnInput) emit("  const u32 u%s = pft3(o%s, p%s);\n", i, i, i);
+            else if (S.kk[j] == kKnPark && (lty(S.kp[j]) == kLocSlot || small)) emit("  const u32 u%s = T.lds_ld(%u);\n", i, lrow(S.kp[j]));
+            else if (S.kk[j] == kKnPark) emit("  const u32 u%s = q%s;\n", i, i);
             else if (lty(S.kp[j]) == kLocSlot || small) emit("  const u32 u%s = pft3(o%s, T.lds_ld(%u));\n", i, i, lrow(S.kp[j]));
             else emit("  const u32 u%s = pft3(o%s, q%s);\n", i, i, i);
             if (!small) put(S.kout[j], "o" + id);
@@ -364,7 +372,8 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
                 const char *i = id.c_str();
                 switch (S.ek[e]) {
                     case kErRed: put(S.ed0[e], a); break;
-                    case kErType1: {  // C = t_u (U ^ Cp) ^ Cp
+                    case kErType1:
+                    case kErType1U: {  // C = t_u (U ^ Cp) ^ Cp
                         emit("  const u32 y%s_0 = %s ^ t%s;\n", i, a.c_str(), i);
                         std::string r;
                         for (int bit = 0; bit < 8 && (t_u >> bit); bit++) {
@@ -372,7 +381,12 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
                             if ((t_u >> bit) & 1) r += (r.empty() ? "" : " ^ ") + ("y" + id + "_" + std::to_string(bit));
                         }
                         emit("  const u32 w%s = %s ^ t%s;\n", i, r.empty() ? "0u" : r.c_str(), i);
-                        put(S.ed0[e], "w" + id);
+                        if (S.ek[e] == kErType1U) {  // the partner's U parked, its row out
+                            put(S.ed0[e], "pft3(t" + id + ", w" + id + ")");
+                            put(S.epd[e], "t" + id);
+                        } else {
+                            put(S.ed0[e], "w" + id);
+                        }
                         put(S.ed1[e], "w" + id);
                         break;
                     }

@@ -237,6 +237,11 @@ const DecJitKernel *dec_jit_get(DecJit *j, const ClayHost &h, const GpePattern &
         return !(e && !strcmp(e, "stage"));
     }();
     if (!direct) wb = 4;  // the staged form (measurement only) has 4-column lanes
+    static const bool fuse = [] {  // TEC_DEC_JIT_FUSE=0: no type-1 fusion (measurement)
+        const char *e = tec_knob("TEC_DEC_JIT_FUSE");
+        return !(e && e[0] == '0');
+    }();
+    if (direct && fuse) dec_prog_fuse_type1(P, steps);  // staged rows would need the moved items flushed
     std::string src = dec_fixed_source(P, D, H, steps, G, kPft.t_u[0], direct, wb);
     const size_t lds = dec_fixed_lds(H, G, direct, wb);
     E->state.store(1);

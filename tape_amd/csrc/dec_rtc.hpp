@@ -66,17 +66,17 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
         if (st >= NS) return;
         const DecStep &S = steps[st];
         for (int j = 0; j < NK; j++) {
-            emit("  const VT o%s = T.ld(%u, %u);\n", id2(st, j).c_str(), (unsigned)H.knode[j], S.z);
+            if (S.kk[j] != kKnPark) emit("  const VT o%s = T.ld(%u, %u);\n", id2(st, j).c_str(), (unsigned)H.knode[j], S.z);
             if (S.kk[j] == kKnInput) emit("  const VT p%s = T.ld(%u, %u);\n", id2(st, j).c_str(), S.kp[j] & 0xffu, S.kp[j] >> 8);
         }
         for (int e = 0; e < NE; e++)
-            if (S.ek[e] == kErType1) emit("  const VT t%s = T.ld(%u, %u);\n", id2(st, e).c_str(), S.ep[e] & 0xffu, S.ep[e] >> 8);
+            if (S.ek[e] == kErType1 || S.ek[e] == kErType1U) emit("  const VT t%s = T.ld(%u, %u);\n", id2(st, e).c_str(), S.ep[e] & 0xffu, S.ep[e] >> 8);
     };
     auto scr_loads = [&](int st) {
         if (st >= NS) return;
         const DecStep &S = steps[st];
         for (int j = 0; j < NK; j++)
-            if (S.kk[j] == kKnLoc && lty(S.kp[j]) == kLocScratch) emit("  const VT q%s = T.scr_ld(%u);\n", id2(st, j).c_str(), lix(S.kp[j]));
+            if ((S.kk[j] == kKnLoc || S.kk[j] == kKnPark) && lty(S.kp[j]) == kLocScratch) emit("  const VT q%s = T.scr_ld(%u);\n", id2(st, j).c_str(), lix(S.kp[j]));
         for (int e = 0; e < NE; e++)
             if (S.ek[e] == kErFinish && lty(S.ep[e]) == kLocScratch) emit("  const VT r%s = T.scr_ld(%u);\n", id2(st, e).c_str(), lix(S.ep[e]));
     };
@@ -99,6 +99,11 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
         for (int j = 0; j < NK; j++) {
             const std::string id = id2(st, j);
             const char *i = id.c_str();
+            if (S.kk[j] == kKnPark) {  // U parked by the type-1 step (which also stored the row out)
+                if (lty(S.kp[j]) == kLocSlot) emit("  const VT u%s = T.lds_ld(%u);\n", i, SLOT0 + lix(S.kp[j]));
+                else emit("  const VT u%s = q%s;\n", i, i);
+                continue;
+            }
             emit("  const VT c%s = T.rot(o%s);\n", i, i);
             if (S.kk[j] == kKnRed) emit("  const VT u%s = c%s;\n", i, i);
             else if (S.kk[j] == kKnInput) emit("  const VT u%s = pft3(c%s, T.rot(p%s));\n", i, i, i);
@@ -155,7 +160,8 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
             const char *i = id.c_str();
             switch (S.ek[e]) {
                 case kErRed: put(S.ed0[e], a); break;
-                case kErType1: {  // C = t_u (U ^ Cp) ^ Cp
+                case kErType1:
+                case kErType1U: {  // C = t_u (U ^ Cp) ^ Cp
                     emit("  const VT k%s = T.rot(t%s);\n", i, i);
                     emit("  const VT y%s_0 = %s ^ k%s;\n", i, a.c_str(), i);
                     std::string r;
@@ -164,7 +170,12 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
                         if ((t_u >> bit) & 1) r += (r.empty() ? "" : " ^ ") + ("y" + id + "_" + std::to_string(bit));
                     }
                     emit("  const VT w%s = %s ^ k%s;\n", i, r.empty() ? "VZ" : r.c_str(), i);
-                    put(S.ed0[e], "w" + id);
+                    if (S.ek[e] == kErType1U) {  // the partner's U parked, its row out (direct output only)
+                        put(S.ed0[e], "pft3(k" + id + ", w" + id + ")");
+                        put(S.epd[e], "k" + id);
+                    } else {
+                        put(S.ed0[e], "w" + id);
+                    }
                     put(S.ed1[e], "w" + id);
                     break;
                 }

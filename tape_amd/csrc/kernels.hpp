@@ -151,8 +151,11 @@ constexpr int kDecMaxK = 10, kDecMaxE = 13, kDecMaxOut = 16;
 constexpr int kDecMaxOutProg = 32;  // DecStep items: the packed (table-kernel) form holds kDecMaxOut
 constexpr uint32_t kLocNone = 0xffffffffu;
 enum : uint32_t { kLocStage = 0, kLocSlot = 1, kLocScratch = 2 };
-enum : uint32_t { kKnRed = 0, kKnInput = 1, kKnLoc = 2 };                       // known j kinds
-enum : uint32_t { kErSkip = 0, kErRed = 1, kErType1 = 2, kErPark = 3, kErFinish = 4 };  // erased e kinds
+enum : uint32_t { kKnRed = 0, kKnInput = 1, kKnLoc = 2, kKnPark = 3 };                       // known j kinds
+enum : uint32_t { kErSkip = 0, kErRed = 1, kErType1 = 2, kErPark = 3, kErFinish = 4, kErType1U = 5 };  // erased e kinds
+// kKnPark / kErType1U (generated class kernels and hipRTC pattern kernels, dec_prog_fuse_type1): the type-1 step
+// parks its known partner's U = pft3(Cp, C) instead of C, and stores the partner's row out if it is
+// an output, so the partner's own step reads U from the location and never loads its own row.
 struct DecStep {
     uint32_t z;                    // plane
     uint32_t nout;                 // flush items (item i = staging row i)

@@ -36,16 +36,25 @@ struct Prog {
 };
 
 // Interpret class `id`'s program on pattern P (physical).  Returns false on a wrong byte.
+// id < 0: a pattern's own program (ClayHost::dec_prog, physical nodes and planes, data output),
+// as the hipRTC pattern kernels run it
 static bool run(const Prog &pg, int id, const GpePattern &P, const uint8_t *chunks, size_t cs, size_t sc, int lost) {
-    const DecClassSpec s = dec_class_spec(id);
+    const DecClassSpec s = dec_class_spec(id < 0 ? 0 : id);
     const int NK = (int)P.nknown, NE = (int)P.nerased;
     auto phys = [&](int c) {
+        if (id < 0) return c;
         const auto sl = dec_class_slot(s, c);
         return sl.first ? (int)P.known[sl.second] : (int)P.erased[sl.second];
     };
-    auto kidx = [&](int c) { return dec_class_slot(s, c).second; };
+    auto kidx = [&](int c) {
+        if (id >= 0) return dec_class_slot(s, c).second;
+        for (int j = 0; j < NK; j++)
+            if ((int)P.known[j] == c) return j;
+        return 0;
+    };
     // a wrong program (the negative check) can map a digit to the other column: -1, never indexed
     auto plane = [&](uint32_t z) {
+        if (id < 0) return (int)z;
         const int d0 = phys((int)z / 10), d1 = phys(10 + (int)z % 10) - 10;
         return d0 >= 0 && d0 < 10 && d1 >= 0 && d1 < 10 ? d0 * 10 + d1 : -1;
     };
@@ -91,6 +100,10 @@ static bool run(const Prog &pg, int id, const GpePattern &P, const uint8_t *chun
             uint8_t u[kDecMaxK], v[kDecMaxE] = {};
             for (int j = 0; j < NK; j++) {
                 const uint8_t o = in((int)P.known[j], zp, b);
+                if (S.kk[j] == kKnPark) {  // U parked by the type-1 step; the row is not read here
+                    u[j] = get(S.kp[j]);
+                    continue;
+                }
                 if (S.kk[j] == kKnRed) u[j] = o;
                 else if (S.kk[j] == kKnInput) u[j] = pft3(o, in((int)P.known[kidx((int)(S.kp[j] & 0xffu))], plane(S.kp[j] >> 8), b));
                 else u[j] = pft3(o, get(S.kp[j]));
@@ -104,10 +117,16 @@ static bool run(const Prog &pg, int id, const GpePattern &P, const uint8_t *chun
                 for (int j = 0; j < NK; j++) a ^= mul4(P.D4[e][j], u[j]);
                 switch (S.ek[e]) {
                     case kErRed: put(S.ed0[e], a); break;
-                    case kErType1: {
+                    case kErType1:
+                    case kErType1U: {
                         const uint8_t k = in((int)P.known[kidx((int)(S.ep[e] & 0xffu))], plane(S.ep[e] >> 8), b);
                         const uint8_t w = (uint8_t)(gf_mul(kPft.t_u[0], (uint8_t)(a ^ k)) ^ k);
-                        put(S.ed0[e], w);
+                        if (S.ek[e] == kErType1U) {
+                            put(S.ed0[e], pft3(k, w));
+                            put(S.epd[e], k);
+                        } else {
+                            put(S.ed0[e], w);
+                        }
                         put(S.ed1[e], w);
                         break;
                     }
@@ -180,6 +199,26 @@ int main(int argc, char **argv) {
                 }
             }
     }
+    // the patterns' own programs with the type-1 fusion (the hipRTC kernels' form): every 61st
+    // erasure set of every size 1..13, both row orientations
+    long plain = 0, plain_fused = 0;
+    for (uint32_t m = 1, seen_p = 0; m < (1u << 20); m++) {
+        const int ne = __builtin_popcount(m);
+        if (ne > 13 || seen_p++ % 61) continue;
+        GpePattern P;
+        pool.clear();
+        if (!h.gpe_pattern(h.pad_erasures(m), P, pool)) return 2;
+        for (int orient = 0; orient < 2; orient++) {
+            Prog pg;
+            if (!h.dec_prog(P, orient, pg.H, pg.steps)) continue;
+            plain_fused += dec_prog_fuse_type1(P, pg.steps);
+            plain++;
+            if (!run(pg, -1, P, chunks.data(), cs, sc, -1)) {
+                printf("FAIL pattern program mask %05x orient %d\n", m, orient);
+                bad++;
+            }
+        }
+    }
     // the check can fail: the neighbouring class's program on a pattern must not reproduce it
     long caught = 0, tried = 0;
     long seen = 0;
@@ -196,7 +235,8 @@ int main(int argc, char **argv) {
         printf("FAIL a wrong class program passed (%ld of %ld caught)\n", caught, tried);
         return 1;
     }
-    printf("sets %ld recover %ld bad %ld wrong-class caught %ld/%ld counts", sets, rec_runs, bad, caught, tried);
+    printf("sets %ld recover %ld patterns %ld (fused pairs %ld) bad %ld wrong-class caught %ld/%ld counts", sets, rec_runs,
+           plain, plain_fused, bad, caught, tried);
     for (int id = 0; id < kDecClasses; id++) printf(" %ld", count[id]);
     printf("\n");
     return bad ? 1 : 0;
