@@ -148,8 +148,10 @@ struct ClayHost {
     // re-encoded); pairs of erased nodes neither of which is output are skipped either way.
     // out_mask != 0 (decode class kernels): the output nodes are exactly those of the mask (items
     // keep their node ids); the kernel drops the outputs that are not data rows.
+    // fuse_pairs (generated kernels only): known pairs coupled within a row of planes as kKnInputU /
+    // kKnPark (kernels.hpp).
     bool dec_prog(const GpePattern &P, int orient, DecProgHdr &H, std::vector<DecStep> &out, int out_node = -1,
-                  uint64_t out_mask = 0) const {
+                  uint64_t out_mask = 0, bool fuse_pairs = false) const {
         if (q != kRepQ || t != 2 || nu != 0 || alpha != kRepQ * kRepQ) return false;
         if (P.nknown > (uint32_t)kDecMaxK || P.nerased > (uint32_t)kDecMaxE) return false;
         const uint64_t em = P.erased_mask;
@@ -175,7 +177,7 @@ struct ClayHost {
         // values: (kind 0 = C / 1 = U, node, plane) -> producer / consumer step (flat index: this
         // runs once per new pattern on the decode path, where random survivor sets are the norm)
         struct Val { int prod = -1, cons = -1; uint32_t loc = kLocNone; };
-        std::vector<int> vid((size_t)2 * qt * alpha, -1);
+        std::vector<int> vid((size_t)3 * qt * alpha, -1);  // kinds: C, U of an erased node, U of a known one
         std::vector<Val> vals;
         vals.reserve(512);
         auto val = [&](int kind, int node, int z) {
@@ -195,7 +197,7 @@ struct ClayHost {
             const int z = order[st];
             DecStep &S = out[st];
             S.z = (uint32_t)z;
-            for (int i = 0; i < kDecMaxK; i++) S.kk[i] = kKnRed, S.kp[i] = 0, S.kout[i] = kLocNone;
+            for (int i = 0; i < kDecMaxK; i++) S.kk[i] = kKnRed, S.kp[i] = 0, S.kout[i] = S.kpark[i] = S.kpout[i] = kLocNone;
             for (int i = 0; i < kDecMaxE; i++) S.ek[i] = kErSkip, S.ep[i] = 0, S.ed0[i] = S.ed1[i] = S.epd[i] = kLocNone;
             auto add_out = [&](int node, int plane) -> uint32_t {
                 if (S.nout >= (uint32_t)kDecMaxOutProg) return kLocNone;
@@ -205,12 +207,28 @@ struct ClayHost {
             bool ok = true;
             for (uint32_t j = 0; j < P.nknown; j++) {
                 const int N = P.known[j], x = N % q, y = N / q, zy = digit(z, y);
+                const int M = y * q + zy, zsw = z + (x - zy) * (int)qpow[t - 1 - y];
+                const bool row_pair = fuse_pairs && zy != x && !er(M) && pos[zsw] / q == st / q;
+                if (row_pair && pos[zsw] < st) {  // the pair's first step parked this U and stored the row
+                    const int v = val(2, N, z);
+                    if (vals[v].prod < 0 || vals[v].cons >= 0) return false;
+                    vals[v].cons = st;
+                    S.kk[j] = kKnPark;
+                    pl.push_back({&S.kp[j], v});
+                    continue;
+                }
                 if (isdata(N)) { S.kout[j] = add_out(N, z); ok = ok && S.kout[j] != kLocNone; }
                 if (zy == x) { S.kk[j] = kKnRed; continue; }
-                const int M = y * q + zy, zsw = z + (x - zy) * (int)qpow[t - 1 - y];
                 if (!er(M)) {
                     S.kk[j] = kKnInput;
                     S.kp[j] = (uint32_t)M | ((uint32_t)zsw << 8);
+                    if (row_pair) {  // first of the pair: the partner's U and row too
+                        S.kk[j] = kKnInputU;
+                        const int v = val(2, M, zsw);
+                        vals[v].prod = st;
+                        pl.push_back({&S.kpark[j], v});
+                        if (isdata(M)) { S.kpout[j] = add_out(M, zsw); ok = ok && S.kpout[j] != kLocNone; }
+                    }
                 } else {
                     const int v = val(0, M, zsw);  // C of the erased partner, recovered earlier
                     if (vals[v].cons >= 0) return false;

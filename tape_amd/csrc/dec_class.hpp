@@ -104,7 +104,7 @@ inline uint64_t dec_class_emask(const DecClassSpec &s) {
 // Program of class `id`'s representative: of the two row orientations the one with fewer
 // scratch rows (HBM traffic), then fewer MDS rows (VALU), within the LDS of two workgroups per CU.
 inline bool dec_class_prog(const ClayHost &h, int id, GpePattern &P, DecProgHdr &H, std::vector<DecStep> &steps,
-                           bool fuse = true) {
+                           bool fuse = true, bool pairs = true) {
     const DecClassSpec s = dec_class_spec(id);
     std::vector<uint16_t> pool;
     if (s.a0 < 0 || !h.gpe_pattern(dec_class_emask(s), P, pool)) return false;
@@ -114,7 +114,7 @@ inline bool dec_class_prog(const ClayHost &h, int id, GpePattern &P, DecProgHdr 
         DecProgHdr H1;
         std::vector<DecStep> st;
         const uint64_t out_mask = s.yl < 0 ? kDecClassOutMask : 1ull << (s.yl == 0 ? s.a0 : 10 + (kDecClassK - s.a0));
-        if (!h.dec_prog(P, orient, H1, st, -1, out_mask)) continue;
+        if (!h.dec_prog(P, orient, H1, st, -1, out_mask, pairs)) continue;
         uint64_t rows = 0;
         for (const DecStep &S : st)
             for (uint32_t e = 0; e < P.nerased; e++) rows += S.ek[e] != kErSkip;
@@ -144,7 +144,8 @@ struct DecClassGenOpt {
     bool tab4 = true;  // 2-bit-field product tables (PermTab4); false: the 3/3/2-bit PermTab
     int own_aux = 2;   // cache policy of the batch kernel's own-row loads (2: non-temporal)
     int scr_aux = 0;   // ... and of its scratch loads (each scratch row is read once)
-    bool fuse = true;  // dec_class_fuse_type1
+    bool fuse = true;   // dec_prog_fuse_type1
+    bool pairs = true;  // dec_prog fuse_pairs
 };
 
 inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecProgHdr &Hout,
@@ -152,7 +153,7 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
     GpePattern P;
     DecProgHdr H;
     std::vector<DecStep> steps;
-    if (!dec_class_prog(h, id, P, H, steps, opt.fuse)) return std::string();
+    if (!dec_class_prog(h, id, P, H, steps, opt.fuse, opt.pairs)) return std::string();
     Hout = H;
     const DecClassSpec cs = dec_class_spec(id);
     const int NK = (int)P.nknown, NE = (int)P.nerased, NS = (int)steps.size();
@@ -189,7 +190,7 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
     uint32_t nring = 1;
     for (const DecStep &S : steps) {
         uint32_t c = 0;
-        for (int j = 0; j < NK; j++) c += (S.kk[j] != kKnPark) + (S.kk[j] == kKnInput);
+        for (int j = 0; j < NK; j++) c += (S.kk[j] != kKnPark) + (S.kk[j] == kKnInput || S.kk[j] == kKnInputU);
         for (int e = 0; e < NE; e++) c += S.ek[e] == kErType1 || S.ek[e] == kErType1U;
         nring = std::max(nring, c);
     }
@@ -229,7 +230,7 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
         for (int j = 0; j < NK; j++)
             if (S.kk[j] != kKnPark) L.push_back("T.ld_own(kb" + std::to_string(j) + ", " + poff(S.z) + ")");
         for (int j = 0; j < NK; j++)
-            if (S.kk[j] == kKnInput) L.push_back("T.ld(kb" + std::to_string(kidx((int)(S.kp[j] & 0xffu))) + ", " + poff(S.kp[j] >> 8) + ")");
+            if (S.kk[j] == kKnInput || S.kk[j] == kKnInputU) L.push_back("T.ld(kb" + std::to_string(kidx((int)(S.kp[j] & 0xffu))) + ", " + poff(S.kp[j] >> 8) + ")");
         for (int e = 0; e < NE; e++)
             if (S.ek[e] == kErType1 || S.ek[e] == kErType1U) L.push_back("T.ld(kb" + std::to_string(kidx((int)(S.ep[e] & 0xffu))) + ", " + poff(S.ep[e] >> 8) + ")");
         return L;
@@ -252,7 +253,7 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
         for (int j = 0; j < NK; j++) {
             if (S.kk[j] != kKnPark)
                 emit("  const u32 o%s = T.ld_aux<%d>(kb%d, %s);\n", id2(st, j).c_str(), opt.own_aux, j, poff(S.z).c_str());
-            if (S.kk[j] == kKnInput)
+            if (S.kk[j] == kKnInput || S.kk[j] == kKnInputU)
                 emit("  const u32 p%s = T.ld(kb%d, %s);\n", id2(st, j).c_str(), kidx((int)(S.kp[j] & 0xffu)),
                      poff(S.kp[j] >> 8).c_str());
         }
@@ -311,7 +312,7 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
             for (int j = 0; j < NK; j++)
                 if (S0.kk[j] != kKnPark) emit("  const u32 o%s = T.lds_ld(%u);\n", id2(st, j).c_str(), ring_row(st, i++));
             for (int j = 0; j < NK; j++)
-                if (S0.kk[j] == kKnInput) emit("  const u32 p%s = T.lds_ld(%u);\n", id2(st, j).c_str(), ring_row(st, i++));
+                if (S0.kk[j] == kKnInput || S0.kk[j] == kKnInputU) emit("  const u32 p%s = T.lds_ld(%u);\n", id2(st, j).c_str(), ring_row(st, i++));
             for (int e = 0; e < NE; e++)
                 if (S0.ek[e] == kErType1 || S0.ek[e] == kErType1U) emit("  const u32 t%s = T.lds_ld(%u);\n", id2(st, e).c_str(), ring_row(st, i++));
             // loader: step st + depth's global loads, step st + 1's rows into the other slot
@@ -325,7 +326,7 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
             const std::string id = id2(st, j);
             const char *i = id.c_str();
             if (S.kk[j] == kKnRed) emit("  const u32 u%s = o%s;\n", i, i);
-            else if (S.kk[j] == kKnInput) emit("  const u32 u%s = pft3(o%s, p%s);\n", i, i, i);
+            else if (S.kk[j] == kKnInput || S.kk[j] == kKnInputU) emit("  const u32 u%s = pft3(o%s, p%s);\n", i, i, i);
             else if (S.kk[j] == kKnPark && (lty(S.kp[j]) == kLocSlot || small)) emit("  const u32 u%s = T.lds_ld(%u);\n", i, lrow(S.kp[j]));
             else if (S.kk[j] == kKnPark) emit("  const u32 u%s = q%s;\n", i, i);
             else if (lty(S.kp[j]) == kLocSlot || small) emit("  const u32 u%s = pft3(o%s, T.lds_ld(%u));\n", i, i, lrow(S.kp[j]));
@@ -339,14 +340,25 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
             if (lty(S.ep[e]) == kLocSlot || small) emit("  const u32 v%s = T.lds_ld(%u);\n", id.c_str(), lrow(S.ep[e]));
             else emit("  const u32 v%s = r%s;\n", id.c_str(), id.c_str());
         }
+        // in-row known pairs: the partner's U parked, its row out -- after every read of the step
+        // (a location is reusable from its consumer step on)
+        auto pair_puts = [&](int j) {
+            if (S.kk[j] != kKnInputU) return;
+            const std::string id = id2(st, j);
+            put(S.kpark[j], "pft3(p" + id + ", o" + id + ")");
+            put(S.kpout[j], "p" + id);
+        };
+        if (!small)
+            for (int j = 0; j < NK; j++) pair_puts(j);
         if (small) {
             // every wave has read what this step reads before any wave writes (a location is
             // reused from its consumer step on); the known rows' copies, spread over the waves
             s += "  T.sync();\n";
             for (int j = 0; j < NK; j++)
-                if (S.kout[j] != kLocNone) {
+                if (S.kout[j] != kLocNone || S.kk[j] == kKnInputU) {
                     emit("  if (T.wv == %du) {\n", j % W);
                     put(S.kout[j], "o" + id2(st, j));
+                    pair_puts(j);
                     s += "  }\n";
                 }
         }

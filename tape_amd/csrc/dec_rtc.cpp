@@ -224,7 +224,16 @@ const DecJitKernel *dec_jit_get(DecJit *j, const ClayHost &h, const GpePattern &
     std::vector<DecStep> steps;
     std::vector<int> known, erased;
     Mat Dm;
-    if (!h.dec_prog(P, orient, H, steps) || !h.decoder(P.erased_mask, known, erased, Dm) ||
+    static const bool direct = [] {  // TEC_DEC_JIT_OUT=stage: rows staged in LDS, flushed whole (measurement)
+        const char *e = tec_knob("TEC_DEC_JIT_OUT");
+        return !(e && !strcmp(e, "stage"));
+    }();
+    static const bool fuse = [] {  // TEC_DEC_JIT_FUSE=0: no type-1 / in-row pair fusion (measurement)
+        const char *e = tec_knob("TEC_DEC_JIT_FUSE");
+        return !(e && e[0] == '0');
+    }();
+    // the fused forms move output rows between steps: direct output only
+    if (!h.dec_prog(P, orient, H, steps, -1, 0, direct && fuse) || !h.decoder(P.erased_mask, known, erased, Dm) ||
         known.size() != P.nknown || erased.size() != P.nerased) {
         E->state.store(-1);
         return nullptr;
@@ -232,16 +241,8 @@ const DecJitKernel *dec_jit_get(DecJit *j, const ClayHost &h, const GpePattern &
     uint8_t D[kGpeMaxErased][kGpeMaxKnown] = {};
     for (size_t e = 0; e < erased.size(); e++)
         for (size_t k = 0; k < known.size(); k++) D[e][k] = Dm.v[e][k];
-    static const bool direct = [] {  // TEC_DEC_JIT_OUT=stage: rows staged in LDS, flushed whole (measurement)
-        const char *e = tec_knob("TEC_DEC_JIT_OUT");
-        return !(e && !strcmp(e, "stage"));
-    }();
     if (!direct) wb = 4;  // the staged form (measurement only) has 4-column lanes
-    static const bool fuse = [] {  // TEC_DEC_JIT_FUSE=0: no type-1 fusion (measurement)
-        const char *e = tec_knob("TEC_DEC_JIT_FUSE");
-        return !(e && e[0] == '0');
-    }();
-    if (direct && fuse) dec_prog_fuse_type1(P, steps);  // staged rows would need the moved items flushed
+    if (direct && fuse) dec_prog_fuse_type1(P, steps);
     std::string src = dec_fixed_source(P, D, H, steps, G, kPft.t_u[0], direct, wb);
     const size_t lds = dec_fixed_lds(H, G, direct, wb);
     E->state.store(1);

@@ -67,7 +67,7 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
         const DecStep &S = steps[st];
         for (int j = 0; j < NK; j++) {
             if (S.kk[j] != kKnPark) emit("  const VT o%s = T.ld(%u, %u);\n", id2(st, j).c_str(), (unsigned)H.knode[j], S.z);
-            if (S.kk[j] == kKnInput) emit("  const VT p%s = T.ld(%u, %u);\n", id2(st, j).c_str(), S.kp[j] & 0xffu, S.kp[j] >> 8);
+            if (S.kk[j] == kKnInput || S.kk[j] == kKnInputU) emit("  const VT p%s = T.ld(%u, %u);\n", id2(st, j).c_str(), S.kp[j] & 0xffu, S.kp[j] >> 8);
         }
         for (int e = 0; e < NE; e++)
             if (S.ek[e] == kErType1 || S.ek[e] == kErType1U) emit("  const VT t%s = T.ld(%u, %u);\n", id2(st, e).c_str(), S.ep[e] & 0xffu, S.ep[e] >> 8);
@@ -106,7 +106,7 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
             }
             emit("  const VT c%s = T.rot(o%s);\n", i, i);
             if (S.kk[j] == kKnRed) emit("  const VT u%s = c%s;\n", i, i);
-            else if (S.kk[j] == kKnInput) emit("  const VT u%s = pft3(c%s, T.rot(p%s));\n", i, i, i);
+            else if (S.kk[j] == kKnInput || S.kk[j] == kKnInputU) emit("  const VT u%s = pft3(c%s, T.rot(p%s));\n", i, i, i);
             else if (lty(S.kp[j]) == kLocSlot) emit("  const VT u%s = pft3(c%s, T.lds_ld(%u));\n", i, i, SLOT0 + lix(S.kp[j]));
             else emit("  const VT u%s = pft3(c%s, q%s);\n", i, i, i);
             put(S.kout[j], "c" + id);
@@ -117,6 +117,14 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
             const std::string id = id2(st, e);
             if (lty(S.ep[e]) == kLocSlot) emit("  const VT v%s = T.lds_ld(%u);\n", id.c_str(), SLOT0 + lix(S.ep[e]));
             else emit("  const VT v%s = r%s;\n", id.c_str(), id.c_str());
+        }
+        // in-row known pairs (direct output only): the partner's U parked, its row out, after the
+        // step's reads
+        for (int j = 0; j < NK; j++) {
+            if (S.kk[j] != kKnInputU) continue;
+            const std::string id = id2(st, j);
+            put(S.kpark[j], "pft3(T.rot(p" + id + "), c" + id + ")");
+            put(S.kpout[j], "T.rot(p" + id + ")");
         }
         // MDS: the erased U's this step needs, j-major over xtime multiples, XOR3 pairs
         std::vector<std::string> acc(NE), pend(NE);

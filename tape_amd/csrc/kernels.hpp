@@ -151,11 +151,14 @@ constexpr int kDecMaxK = 10, kDecMaxE = 13, kDecMaxOut = 16;
 constexpr int kDecMaxOutProg = 32;  // DecStep items: the packed (table-kernel) form holds kDecMaxOut
 constexpr uint32_t kLocNone = 0xffffffffu;
 enum : uint32_t { kLocStage = 0, kLocSlot = 1, kLocScratch = 2 };
-enum : uint32_t { kKnRed = 0, kKnInput = 1, kKnLoc = 2, kKnPark = 3 };                       // known j kinds
+enum : uint32_t { kKnRed = 0, kKnInput = 1, kKnLoc = 2, kKnPark = 3, kKnInputU = 4 };                       // known j kinds
 enum : uint32_t { kErSkip = 0, kErRed = 1, kErType1 = 2, kErPark = 3, kErFinish = 4, kErType1U = 5 };  // erased e kinds
 // kKnPark / kErType1U (generated class kernels and hipRTC pattern kernels, dec_prog_fuse_type1): the type-1 step
 // parks its known partner's U = pft3(Cp, C) instead of C, and stores the partner's row out if it is
 // an output, so the partner's own step reads U from the location and never loads its own row.
+// kKnInputU (dec_prog fuse_pairs): of two known nodes coupled within one row of planes, the first
+// step parks the second's U = pft3(Cp, C) in an LDS slot (kpark) and stores its row out (kpout);
+// the second step is kKnPark and loads neither row.
 struct DecStep {
     uint32_t z;                    // plane
     uint32_t nout;                 // flush items (item i = staging row i)
@@ -163,6 +166,8 @@ struct DecStep {
     uint32_t kk[kDecMaxK];         // known j kind
     uint32_t kp[kDecMaxK];         // kKnInput: partner node | plane << 8; kKnLoc: partner C location
     uint32_t kout[kDecMaxK];       // staging row of the known node's C (data nodes), or none
+    uint32_t kpark[kDecMaxK];      // kKnInputU: location of the partner's U; kpout: its row's output
+    uint32_t kpout[kDecMaxK];
     uint32_t ek[kDecMaxE];         // erased e kind
     uint32_t ep[kDecMaxE];         // type-1: partner node | plane << 8; park: U location; finish: partner U location
     uint32_t ed0[kDecMaxE], ed1[kDecMaxE];  // destinations of C (red / type-1 / finish)

@@ -98,6 +98,8 @@ static bool run(const Prog &pg, int id, const GpePattern &P, const uint8_t *chun
                 return (ty == kLocSlot ? slot_ok : scr_ok)[ix] ? (ty == kLocSlot ? slot : scr)[ix] : (uint8_t)0x5A;
             };
             uint8_t u[kDecMaxK], v[kDecMaxE] = {};
+            struct Pend { int j; uint8_t p, o; };
+            std::vector<Pend> pend;
             for (int j = 0; j < NK; j++) {
                 const uint8_t o = in((int)P.known[j], zp, b);
                 if (S.kk[j] == kKnPark) {  // U parked by the type-1 step; the row is not read here
@@ -105,12 +107,20 @@ static bool run(const Prog &pg, int id, const GpePattern &P, const uint8_t *chun
                     continue;
                 }
                 if (S.kk[j] == kKnRed) u[j] = o;
-                else if (S.kk[j] == kKnInput) u[j] = pft3(o, in((int)P.known[kidx((int)(S.kp[j] & 0xffu))], plane(S.kp[j] >> 8), b));
+                else if (S.kk[j] == kKnInput || S.kk[j] == kKnInputU) {
+                    const uint8_t pv = in((int)P.known[kidx((int)(S.kp[j] & 0xffu))], plane(S.kp[j] >> 8), b);
+                    u[j] = pft3(o, pv);
+                    if (S.kk[j] == kKnInputU) pend.push_back({j, pv, o});
+                }
                 else u[j] = pft3(o, get(S.kp[j]));
                 put(S.kout[j], o);
             }
             for (int e = 0; e < NE; e++)
                 if (S.ek[e] == kErFinish) v[e] = get(S.ep[e]);
+            for (const auto &q : pend) {  // in-row pairs, after the step's reads
+                put(S.kpark[q.j], pft3(q.p, q.o));
+                put(S.kpout[q.j], q.p);
+            }
             for (int e = 0; e < NE; e++) {
                 if (S.ek[e] == kErSkip) continue;
                 uint8_t a = 0;
@@ -199,7 +209,7 @@ int main(int argc, char **argv) {
                 }
             }
     }
-    // the patterns' own programs with the type-1 fusion (the hipRTC kernels' form): every 61st
+    // the patterns' own programs with the in-row pair and type-1 fusions (the hipRTC kernels' form): every 61st
     // erasure set of every size 1..13, both row orientations
     long plain = 0, plain_fused = 0;
     for (uint32_t m = 1, seen_p = 0; m < (1u << 20); m++) {
@@ -210,7 +220,7 @@ int main(int argc, char **argv) {
         if (!h.gpe_pattern(h.pad_erasures(m), P, pool)) return 2;
         for (int orient = 0; orient < 2; orient++) {
             Prog pg;
-            if (!h.dec_prog(P, orient, pg.H, pg.steps)) continue;
+            if (!h.dec_prog(P, orient, pg.H, pg.steps, -1, 0, true)) continue;
             plain_fused += dec_prog_fuse_type1(P, pg.steps);
             plain++;
             if (!run(pg, -1, P, chunks.data(), cs, sc, -1)) {
