@@ -2,7 +2,8 @@
 # Decode class-kernel library variants (scripts/build_class_var.sh -> varlib/lib_<name>.so) against
 # the shipped library and the table-driven kernel: random-pattern and worst-case (hipRTC off)
 # decode lines, interleaved.   usage: VARS="late wpe6" scripts/gpu_class_var.sh <outdir-name>
-# TESTS=1: the decode / recover GPU tests first; JIT=1: the hipRTC worst case, fused and not
+# TESTS=1: the decode / recover GPU tests first; JIT=1: the hipRTC worst case, base and with the
+# knobs in JIT_ALT (default TEC_DEC_JIT_FUSE=0)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/${1:-class_var}
@@ -27,7 +28,7 @@ done
 if [ "${JIT:-0}" == "1" ]; then  # worst case on the hipRTC pattern kernels (after their compile), fused vs not
   for r in 1 2; do
     timeout -k 10 300 env TEC_DEBUG_KNOBS=0 $B > $O/jit_base_$r.json 2> $O/jit_base_$r.err || exit $?
-    timeout -k 10 300 env TEC_DEBUG_KNOBS=1 TEC_DEC_JIT_FUSE=0 $B > $O/jit_nofuse_$r.json 2> $O/jit_nofuse_$r.err || exit $?
+    timeout -k 10 300 env TEC_DEBUG_KNOBS=1 ${JIT_ALT:-TEC_DEC_JIT_FUSE=0} $B > $O/jit_alt_$r.json 2> $O/jit_alt_$r.err || exit $?
   done
 fi
 python3 - $O <<'PY'

@@ -146,6 +146,7 @@ struct DecClassGenOpt {
     int scr_aux = 0;   // ... and of its scratch loads (each scratch row is read once)
     bool fuse = true;   // dec_prog_fuse_type1
     bool pairs = true;  // dec_prog fuse_pairs
+    bool tu_perm = true;  // type-1 coefficient as a v_perm table product (false: xtime chain)
 };
 
 inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecProgHdr &Hout,
@@ -166,6 +167,7 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
     auto lty = [](uint32_t loc) { return loc >> 24; };
     auto lix = [](uint32_t loc) { return loc & 0xffffffu; };
     auto id2 = [](int a, int c) { return std::to_string(a) + "_" + std::to_string(c); };
+    const PermTab tu_tab = perm_tab(t_u);
     // a canonical node as the expression of its physical id
     auto phys = [&](int c) {
         const auto sl = dec_class_slot(cs, c);
@@ -386,13 +388,20 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
                     case kErRed: put(S.ed0[e], a); break;
                     case kErType1:
                     case kErType1U: {  // C = t_u (U ^ Cp) ^ Cp
-                        emit("  const u32 y%s_0 = %s ^ t%s;\n", i, a.c_str(), i);
-                        std::string r;
-                        for (int bit = 0; bit < 8 && (t_u >> bit); bit++) {
-                            if (bit) emit("  const u32 y%s_%d = xt(y%s_%d);\n", i, bit, i, bit - 1);
-                            if ((t_u >> bit) & 1) r += (r.empty() ? "" : " ^ ") + ("y" + id + "_" + std::to_string(bit));
+                        // t_u * y as a v_perm table product of compile-time tables (~10 VALU;
+                        // the xtime chain of t_u = 0xf4 was ~37)
+                        if (opt.tu_perm) {
+                            emit("  const u32 w%s = perm_mul_acc(t%s, Sel(%s ^ t%s), 0x%08xu, 0x%08xu, 0x%08xu, 0x%08xu, 0x%08xu);\n",
+                                 i, i, a.c_str(), i, tu_tab.t[0], tu_tab.t[1], tu_tab.t[2], tu_tab.t[3], tu_tab.t[4]);
+                        } else {  // the xtime chain
+                            emit("  const u32 y%s_0 = %s ^ t%s;\n", i, a.c_str(), i);
+                            std::string r;
+                            for (int bit = 0; bit < 8 && (t_u >> bit); bit++) {
+                                if (bit) emit("  const u32 y%s_%d = xt(y%s_%d);\n", i, bit, i, bit - 1);
+                                if ((t_u >> bit) & 1) r += (r.empty() ? "" : " ^ ") + ("y" + id + "_" + std::to_string(bit));
+                            }
+                            emit("  const u32 w%s = %s ^ t%s;\n", i, r.empty() ? "0u" : r.c_str(), i);
                         }
-                        emit("  const u32 w%s = %s ^ t%s;\n", i, r.empty() ? "0u" : r.c_str(), i);
                         if (S.ek[e] == kErType1U) {  // the partner's U parked, its row out
                             put(S.ed0[e], "pft3(t" + id + ", w" + id + ")");
                             put(S.epd[e], "t" + id);

@@ -48,6 +48,12 @@ TEC_DFI u32 xt(u32 x) {
     return ((x & 0x7f7f7f7fu) << 1) ^ __builtin_amdgcn_perm(0u, 0x00001d00u, hb);
 }
 TEC_DFI u32 pft3(u32 a, u32 b) { return a ^ xt(a ^ b); }  // 3a ^ 2b: U from (C, C_partner), C from (U, U_partner)
+// c * x for a constant c given as its 3/3/2-bit v_perm tables (gf.hpp PermTab): ~9 VALU where an
+// xtime chain of c = 0xf4 (the type-1 coefficient) is ~37
+TEC_DFI u32 mulk(u32 x, u32 t0, u32 t1, u32 t2, u32 t3, u32 t4) {
+    return xor3(__builtin_amdgcn_perm(t1, t0, x & 0x07070707u), __builtin_amdgcn_perm(t3, t2, (x >> 3) & 0x07070707u),
+                __builtin_amdgcn_perm(t4, t4, (x >> 6) & 0x03030303u));
+}
 
 // A lane's 8 columns (8-byte lanes, WB = 8): two dwords, every operation byte-wise per dword.
 struct V2 {
@@ -57,6 +63,9 @@ TEC_DFI V2 operator^(V2 a, V2 b) { return V2{a.x ^ b.x, a.y ^ b.y}; }
 TEC_DFI V2 xor3(V2 a, V2 b, V2 c) { return V2{xor3(a.x, b.x, c.x), xor3(a.y, b.y, c.y)}; }
 TEC_DFI V2 xt(V2 a) { return V2{xt(a.x), xt(a.y)}; }
 TEC_DFI V2 pft3(V2 a, V2 b) { return a ^ xt(a ^ b); }
+TEC_DFI V2 mulk(V2 x, u32 t0, u32 t1, u32 t2, u32 t3, u32 t4) {
+    return V2{mulk(x.x, t0, t1, t2, t3, t4), mulk(x.y, t0, t1, t2, t3, t4)};
+}
 
 // Lane value type and its memory forms per lane width.
 template <int WB> struct Lane;

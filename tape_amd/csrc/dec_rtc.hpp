@@ -45,6 +45,11 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
     auto lty = [](uint32_t loc) { return loc >> 24; };
     auto lix = [](uint32_t loc) { return loc & 0xffffffu; };
     auto id2 = [](int a, int c) { return std::to_string(a) + "_" + std::to_string(c); };
+    static const bool tu_perm = [] {  // TEC_DEC_JIT_TU=xt: the xtime chain (measurement)
+        const char *e = tec_knob("TEC_DEC_JIT_TU");
+        return !(e && e[0] == 'x');
+    }();
+    const PermTab tu_tab = perm_tab(t_u);
     if (direct) s += "#define TEC_DFIX_RAW 1\n";  // words kept in load order (dec_fixed.hpp Tile::rot)
     s += "#include \"dec_fixed.hpp\"\nusing namespace tec::dfix;\n";
     emit("typedef Lane<%d>::V VT;\n#define VZ (Lane<%d>::zero())\n", wb, wb);
@@ -172,12 +177,17 @@ inline std::string dec_fixed_source(const GpePattern &P, const uint8_t (*D)[kGpe
                 case kErType1U: {  // C = t_u (U ^ Cp) ^ Cp
                     emit("  const VT k%s = T.rot(t%s);\n", i, i);
                     emit("  const VT y%s_0 = %s ^ k%s;\n", i, a.c_str(), i);
-                    std::string r;
-                    for (int bit = 0; bit < 8 && (t_u >> bit); bit++) {
-                        if (bit) emit("  const VT y%s_%d = xt(y%s_%d);\n", i, bit, i, bit - 1);
-                        if ((t_u >> bit) & 1) r += (r.empty() ? "" : " ^ ") + ("y" + id + "_" + std::to_string(bit));
+                    if (tu_perm) {  // t_u * y as a v_perm product of compile-time tables
+                        emit("  const VT w%s = mulk(y%s_0, 0x%08xu, 0x%08xu, 0x%08xu, 0x%08xu, 0x%08xu) ^ k%s;\n", i, i,
+                             tu_tab.t[0], tu_tab.t[1], tu_tab.t[2], tu_tab.t[3], tu_tab.t[4], i);
+                    } else {
+                        std::string r;
+                        for (int bit = 0; bit < 8 && (t_u >> bit); bit++) {
+                            if (bit) emit("  const VT y%s_%d = xt(y%s_%d);\n", i, bit, i, bit - 1);
+                            if ((t_u >> bit) & 1) r += (r.empty() ? "" : " ^ ") + ("y" + id + "_" + std::to_string(bit));
+                        }
+                        emit("  const VT w%s = %s ^ k%s;\n", i, r.empty() ? "VZ" : r.c_str(), i);
                     }
-                    emit("  const VT w%s = %s ^ k%s;\n", i, r.empty() ? "VZ" : r.c_str(), i);
                     if (S.ek[e] == kErType1U) {  // the partner's U parked, its row out (direct output only)
                         put(S.ed0[e], "pft3(k" + id + ", w" + id + ")");
                         put(S.epd[e], "k" + id);
