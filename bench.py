@@ -157,7 +157,7 @@ def config5_rates(total_objects: int, L: int, steps: int, rank_elapsed_s: list, 
 KERNELS = {
     "encode": ["tec::dma::enc_dma_kernel<false>"],
     "repair": ["tec::rfold::rep_fold_kernel"],  # every folded instance (lost column x known set)
-    "decode": ["tec_dec_fixed"],  # the pattern kernels (dec_rtc.cpp); random patterns / --decode-jit off: table-driven
+    "decode": ["tec::dcls::dec_class_"],  # the decode class kernels (decode_class.hip), side by side
     "commit": ["tec::commit::leaf_kernel", "tec::commit::tree_kernel"],
     "recover": ["tec::dcls::dec_class_"],  # the recover class kernels (decode_class.hip), side by side
     "outer": ["tec::rs16k::rs16_matrix_kernel<9, 32, false>"],  # OuterCoder(17, 50) encode: 17 x 33 matrix
@@ -168,10 +168,9 @@ LAUNCHES_PER_STEP = {"outer_decode": 3}
 
 
 def kernel_names(mode: str, decode_jit: str = "async", pattern: str = "worst") -> list:
-    # random survivor sets serve ~1 object per pattern: no pattern reaches a hipRTC kernel, every
-    # stripe runs its class's kernel (decode_class.hip)
-    if mode == "decode" and (decode_jit == "off" or pattern == "random"):
-        return ["tec::dcls::dec_class_"]
+    # Clay(20,7,16) decode, worst case or random survivor sets: every stripe runs its class's kernel
+    # (decode_class.hip); the hipRTC pattern kernels serve other profiles' hot patterns, or callers
+    # that ask for them (te_clay_set_decode_jit)
     return KERNELS.get(mode, [])
 
 

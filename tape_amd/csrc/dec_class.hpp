@@ -374,6 +374,11 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
             for (int e = 0; e < NE; e++) {
                 if (S.ek[e] == kErSkip || own_e[e] != w) continue;
                 const std::string a = "a" + id2(st, e);
+                // decode: a red row whose only use is a column-0 parity node's output (dropped) is
+                // not computed (uniform branch on the relabelled node)
+                const bool drop_red = cs.yl < 0 && S.ek[e] == kErRed && S.ed0[e] != kLocNone &&
+                                      lty(S.ed0[e]) == kLocStage && (S.out[lix(S.ed0[e])] & 0xffu) < 10u;
+                if (drop_red) emit("  if (ob%u != T.kDropBase) {\n", S.out[lix(S.ed0[e])] & 0xffu);
                 emit("  u32 %s = 0u;\n  { const auto D = T.%s();\n", a.c_str(), opt.tab4 ? "mat4" : "mat");
                 for (int j = 0; j + 1 < NK; j += 2)
                     emit("  %s = T.mul2(%s, D, %d, %d, s%s, s%s);\n", a.c_str(), a.c_str(), e, j, id2(st, j).c_str(),
@@ -385,7 +390,10 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
                 const std::string id = id2(st, e);
                 const char *i = id.c_str();
                 switch (S.ek[e]) {
-                    case kErRed: put(S.ed0[e], a); break;
+                    case kErRed:
+                        put(S.ed0[e], a);
+                        if (drop_red) s += "  }\n";
+                        break;
                     case kErType1:
                     case kErType1U: {  // C = t_u (U ^ Cp) ^ Cp
                         // t_u * y as a v_perm table product of compile-time tables (~10 VALU;

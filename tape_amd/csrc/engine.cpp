@@ -1370,6 +1370,10 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     // a caller that lowered the build threshold (te_clay_set_decode_jit, tests) lowers the floor too
     const uint64_t jit_floor = c->jit_mode >= 0 ? std::min<uint64_t>(kJitMinStripes, c->jit_min) : kJitMinStripes;
     std::vector<Fixed> fixed;
+    static const bool class_on = [] {
+        const char *e = tec_knob("TEC_DEC_CLASS");
+        return !(e && e[0] == '0');
+    }();
     if (staged && !fused) {  // (pattern kernels write data chunks; recover's outputs are other nodes)
         if (!c->jit) {
             c->jit = dec_jit_new(c->device);
@@ -1389,6 +1393,11 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
                 // against 14.5 for the shared one).  Such groups do not count toward building a
                 // kernel either: it could never be launched for them.
                 if (cnt[p] < std::max<uint64_t>(1, jit_floor)) continue;
+                // a survivor set with a class kernel runs it: after the load fusions the class
+                // kernels time at or below the hipRTC pattern kernels (4.26 vs 4.36-4.39 ms, worst
+                // case, same box) with no 25 s compile; a caller that asked for the pattern kernels
+                // (te_clay_set_decode_jit) still gets them
+                if (c->jit_mode < 0 && class_on && dec_class_of(h, cached[p]->P) >= 0) continue;
                 const DecJitKernel *k = dec_jit_get(c->jit, h, cached[p]->P, cached[p]->orient, (int)geo.G, (int)geo.wb, cnt[p]);
                 if (!k) continue;
                 fx[p] = (int)fixed.size();
@@ -1408,10 +1417,6 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     // Measurement option TEC_DEBUG_KNOBS=1 TEC_DEC_CLASS=0: the table-driven kernel instead.
     struct ClassGrp { uint64_t key; int id; std::vector<GpeJob> jobs; size_t off = 0; };
     std::vector<ClassGrp> cls;
-    static const bool class_on = [] {
-        const char *e = tec_knob("TEC_DEC_CLASS");
-        return !(e && e[0] == '0');
-    }();
     // streams the class groups of a call run on, side by side (TEC_DEC_CLASS_STREAMS)
     static const int class_streams = [] {
         const char *e = tec_knob("TEC_DEC_CLASS_STREAMS");
