@@ -1417,6 +1417,11 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     // Measurement option TEC_DEBUG_KNOBS=1 TEC_DEC_CLASS=0: the table-driven kernel instead.
     struct ClassGrp { uint64_t key; int id; std::vector<GpeJob> jobs; size_t off = 0; };
     std::vector<ClassGrp> cls;
+    bool cls_small = false;  // the class stripes fit one round of per-call workgroups
+    static const bool small_dec_cls = [] {  // measurement option TEC_DEC_CLASS_SMALL=0: the r06 rule
+        const char *e = tec_knob("TEC_DEC_CLASS_SMALL");
+        return !(e && e[0] == '0');
+    }();
     // streams the class groups of a call run on, side by side (TEC_DEC_CLASS_STREAMS)
     static const int class_streams = [] {
         const char *e = tec_knob("TEC_DEC_CLASS_STREAMS");
@@ -1455,10 +1460,19 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         // classes against 3.00, r06)
         // (per-call decodes of <= 64 stripes run the classes' one-wave kernels, whose input loads
         // lead by four steps: their chains are short enough to run a few one after another)
-        size_t ncls = 0, nall = 0;
-        for (const ClassGrp &cg : cls) ncls += cg.jobs.size();
+        // A call whose class stripes fit one round of per-call workgroups (G = 1: 4 compute waves
+        // and a loader wave per 64-column group, <= 2 per CU by LDS) runs them all on the per-call
+        // kernels instead: each chain is short, so a few launches one after another still cost
+        // less than one table-driven launch (64 MiB per call: 68 stripes, ~5 classes).
+        size_t ncls = 0, nall = 0, small_wgs = 0;
+        for (const ClassGrp &cg : cls) {
+            ncls += cg.jobs.size();
+            const uint64_t sc = (cg.key >> 32) / (uint64_t)h.alpha;
+            small_wgs += cg.jobs.size() * (size_t)((sc / 4 + 63) / 64);
+        }
         for (auto &kv : groups) nall += kv.second.size();
-        if (cls.size() > (size_t)class_streams && ncls < 1024 && ncls + nall > kDecSmallStripes) {
+        cls_small = small_dec_cls && !cls.empty() && small_wgs <= 512;
+        if (!cls_small && cls.size() > (size_t)class_streams && ncls < 1024 && ncls + nall > kDecSmallStripes) {
             for (ClassGrp &cg : cls) groups[cg.key].insert(groups[cg.key].end(), cg.jobs.begin(), cg.jobs.end());
             cls.clear();
         }
@@ -1560,7 +1574,7 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         const char *e = tec_knob("TEC_DEC_CLASS_G");
         return e && atoi(e) == 1 ? 1u : 2u;
     }();
-    const uint32_t class_g = call_stripes <= dec_small_max ? 1u : class_g_big;
+    const uint32_t class_g = call_stripes <= dec_small_max || (cls_small && small_dec_cls) ? 1u : class_g_big;
     const bool small_dec = call_stripes <= dec_small_max;
     auto dec_args = [&](const std::pair<uint64_t, size_t> &o) {
         const uint64_t cs = o.first >> 32;
