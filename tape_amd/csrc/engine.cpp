@@ -1418,9 +1418,11 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
     struct ClassGrp { uint64_t key; int id; std::vector<GpeJob> jobs; size_t off = 0; };
     std::vector<ClassGrp> cls;
     bool cls_small = false;  // the class stripes fit one round of per-call workgroups
-    static const bool small_dec_cls = [] {  // measurement option TEC_DEC_CLASS_SMALL=0: the r06 rule
+    // measurement option TEC_DEC_CLASS_SMALL=1 (off by default: per call 64 MiB, kernel 0.596 ms
+    // on the per-call class kernels against 0.472 on the one table-driven launch)
+    static const bool small_dec_cls = [] {
         const char *e = tec_knob("TEC_DEC_CLASS_SMALL");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     // streams the class groups of a call run on, side by side (TEC_DEC_CLASS_STREAMS)
     static const int class_streams = [] {
@@ -1460,10 +1462,9 @@ int decode_enqueue(te_clay *c, const te_slicer_cfg *cfg, const uint8_t *d_slices
         // classes against 3.00, r06)
         // (per-call decodes of <= 64 stripes run the classes' one-wave kernels, whose input loads
         // lead by four steps: their chains are short enough to run a few one after another)
-        // A call whose class stripes fit one round of per-call workgroups (G = 1: 4 compute waves
-        // and a loader wave per 64-column group, <= 2 per CU by LDS) runs them all on the per-call
-        // kernels instead: each chain is short, so a few launches one after another still cost
-        // less than one table-driven launch (64 MiB per call: 68 stripes, ~5 classes).
+        // (TEC_DEC_CLASS_SMALL=1: a call whose class stripes fit one round of per-call workgroups
+        // -- G = 1, 4 compute waves and a loader wave per 64-column group, <= 2 per CU by LDS --
+        // runs them on the per-call kernels instead; measured slower for 64 MiB per call)
         size_t ncls = 0, nall = 0, small_wgs = 0;
         for (const ClassGrp &cg : cls) {
             ncls += cg.jobs.size();
