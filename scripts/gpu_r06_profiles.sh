@@ -4,13 +4,13 @@
 # side by side on forked streams, the per-call span (first class-kernel start to last end) from the
 # kernel trace (scripts/class_span.py) is what must agree with the line's in-run device time; then
 # the PMC traffic passes of decode:random and recover (scripts/profile_modes.sh).
-#   usage: scripts/gpu_r06_profiles.sh <outdir-name>   (PMC=0 skips the counter passes)
+#   usage: scripts/gpu_r06_profiles.sh <outdir-name>   (PMC=0 skips the counter passes; SPECS="mode[:pattern] ...")
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r06_prof}
 mkdir -p $O
-for spec in encode decode:random recover repair; do
+for spec in ${SPECS:-encode decode:random recover repair}; do
   m=${spec%%:*}; pat=${spec#*:}; [ "$pat" == "$spec" ] && pat=worst
   d=$O/${spec/:/_}
   B="python3 bench.py --mode $m --pattern $pat --steps 10 --warmup 3 --cpu-sample 0 --copy-objects 0 --sdk-chunks 0"

@@ -34,6 +34,10 @@
 #define TEC_RFOLD_WPE 4  // 128 VGPRs (52 B/lane spill): 0.567 ms vs 0.63 at 141 VGPRs (1024 x 4 MiB)
 #endif
 #ifndef TEC_RFOLD_DIRECT
+#ifndef TEC_RFOLD_AP_FOLD
+#define TEC_RFOLD_AP_FOLD 1  // aloof planes' U with one constant product (0: two, measurement)
+#endif
+static_assert(tec::kPft.a_p[0] == (tec::kPft.a_c[0] ^ 1), "a_p = a_c ^ 1 (PFT [[3,2],[2,3]])");
 #define TEC_RFOLD_DIRECT 1  // 1: each finished word stored straight to the lost chunk (no staging, no barrier)
 #endif
 #ifndef TEC_RFOLD_MAXG
@@ -281,7 +285,15 @@ __device__ __forceinline__ void rep_fold_body(const RepArgs &a) {
         __builtin_amdgcn_sched_barrier(0);
         uint32_t u[kK], ccm[kQ], acc[kQ];
 #pragma unroll
-        for (int j = 0; j < kK; j++) u[j] = mulc(kPft.a_c[0], own[j]) ^ mulc(kPft.a_p[0], *ua_at(ip, j));
+        for (int j = 0; j < kK; j++) {
+#if TEC_RFOLD_AP_FOLD
+            // a_c C ^ a_p U with a_p = a_c ^ 1: one table product, a_c (C ^ U) ^ U
+            const uint32_t ua = *ua_at(ip, j);
+            u[j] = mulc(kPft.a_c[0], own[j] ^ ua) ^ ua;
+#else
+            u[j] = mulc(kPft.a_c[0], own[j]) ^ mulc(kPft.a_p[0], *ua_at(ip, j));
+#endif
+        }
 #pragma unroll
         for (int x = 0; x < kQ; x++) ccm[x] = cm[x];
         if (ip + 1 < kA) load_plane((uint32_t)KS.al[ip + 1]);
