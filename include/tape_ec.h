@@ -104,7 +104,9 @@ int te_clay_device(const te_clay *c);
 /* Per-pattern decode kernels (no reference counterpart; an engine knob).  A hot erasure pattern
  * of a q = 10, t = 2 profile gets a kernel with its plane program and decoding matrix compiled
  * in (hipRTC, ~25 s of host time, off the caller's thread in mode 1); until then, and for every
- * other pattern, the table-driven kernel decodes it.  mode: 0 off, 1 async (default; env
+ * other pattern, the table-driven kernel decodes it.  Clay(20,7,16) survivor sets run their
+ * ahead-of-time class kernels instead, which time at or below the pattern kernels, unless this
+ * function has been called on the handle.  mode: 0 off, 1 async (default; env
  * TEC_DEC_JIT=off|sync|async), 2 sync (compile in the decoding call).  A pattern is built once
  * `min_stripes` of its stripes have been decoded on the handle (default 1024, env
  * TEC_DEC_JIT_MIN). */
