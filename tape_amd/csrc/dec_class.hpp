@@ -147,6 +147,8 @@ struct DecClassGenOpt {
     bool fuse = true;   // dec_prog_fuse_type1
     bool pairs = true;  // dec_prog fuse_pairs
     bool tu_perm = true;  // type-1 coefficient as a v_perm table product (false: xtime chain)
+    bool drop_pairs = false;  // decode: skip column-0 pairs whose nodes are both parity (slower: the
+                              // 420 uniform branches per kernel cost more scheduling than the rows)
 };
 
 inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecProgHdr &Hout,
@@ -167,7 +169,7 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
     auto lty = [](uint32_t loc) { return loc >> 24; };
     auto lix = [](uint32_t loc) { return loc & 0xffffffu; };
     auto id2 = [](int a, int c) { return std::to_string(a) + "_" + std::to_string(c); };
-    const PermTab tu_tab = perm_tab(t_u);
+    const PermTab tu_tab = perm_tab(t_u), tu2_tab = perm_tab(gf_mul(2, t_u));
     // a canonical node as the expression of its physical id
     auto phys = [&](int c) {
         const auto sl = dec_class_slot(cs, c);
@@ -379,6 +381,13 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
                 const bool drop_red = cs.yl < 0 && S.ek[e] == kErRed && S.ed0[e] != kLocNone &&
                                       lty(S.ed0[e]) == kLocStage && (S.out[lix(S.ed0[e])] & 0xffu) < 10u;
                 if (drop_red) emit("  if (ob%u != T.kDropBase) {\n", S.out[lix(S.ed0[e])] & 0xffu);
+                // decode: a pair of column-0 nodes (park, then finish at the partner's plane) both
+                // of which are parity nodes feeds nothing but dropped outputs: skipped alike at
+                // both steps (the condition is symmetric in the pair)
+                const int ecan = e < 10 - cs.a0 ? cs.a0 + e : -1;  // canonical column-0 erased node
+                const bool drop_pair = opt.drop_pairs && cs.yl < 0 && ecan >= 0 &&
+                                       (S.ek[e] == kErPark || S.ek[e] == kErFinish);
+                if (drop_pair) emit("  if (ob%d != T.kDropBase || ob%u != T.kDropBase) {\n", ecan, S.z / 10);
                 emit("  u32 %s = 0u;\n  { const auto D = T.%s();\n", a.c_str(), opt.tab4 ? "mat4" : "mat");
                 for (int j = 0; j + 1 < NK; j += 2)
                     emit("  %s = T.mul2(%s, D, %d, %d, s%s, s%s);\n", a.c_str(), a.c_str(), e, j, id2(st, j).c_str(),
@@ -399,8 +408,9 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
                         // t_u * y as a v_perm table product of compile-time tables (~10 VALU;
                         // the xtime chain of t_u = 0xf4 was ~37)
                         if (opt.tu_perm) {
-                            emit("  const u32 w%s = perm_mul_acc(t%s, Sel(%s ^ t%s), 0x%08xu, 0x%08xu, 0x%08xu, 0x%08xu, 0x%08xu);\n",
-                                 i, i, a.c_str(), i, tu_tab.t[0], tu_tab.t[1], tu_tab.t[2], tu_tab.t[3], tu_tab.t[4]);
+                            emit("  const Sel y%s(%s ^ t%s);\n", i, a.c_str(), i);
+                            emit("  const u32 w%s = perm_mul_acc(t%s, y%s, 0x%08xu, 0x%08xu, 0x%08xu, 0x%08xu, 0x%08xu);\n",
+                                 i, i, i, tu_tab.t[0], tu_tab.t[1], tu_tab.t[2], tu_tab.t[3], tu_tab.t[4]);
                         } else {  // the xtime chain
                             emit("  const u32 y%s_0 = %s ^ t%s;\n", i, a.c_str(), i);
                             std::string r;
@@ -410,7 +420,14 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
                             }
                             emit("  const u32 w%s = %s ^ t%s;\n", i, r.empty() ? "0u" : r.c_str(), i);
                         }
-                        if (S.ek[e] == kErType1U) {  // the partner's U parked, its row out
+                        if (S.ek[e] == kErType1U && opt.tu_perm) {
+                            // the partner's U = pft3(Cp, C) = Cp ^ (2 t_u)(U ^ Cp): a second table
+                            // product of the same selectors; its row out
+                            emit("  const u32 x%s = perm_mul_acc(t%s, y%s, 0x%08xu, 0x%08xu, 0x%08xu, 0x%08xu, 0x%08xu);\n",
+                                 i, i, i, tu2_tab.t[0], tu2_tab.t[1], tu2_tab.t[2], tu2_tab.t[3], tu2_tab.t[4]);
+                            put(S.ed0[e], "x" + id);
+                            put(S.epd[e], "t" + id);
+                        } else if (S.ek[e] == kErType1U) {  // the partner's U parked, its row out
                             put(S.ed0[e], "pft3(t" + id + ", w" + id + ")");
                             put(S.epd[e], "t" + id);
                         } else {
@@ -419,10 +436,14 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
                         put(S.ed1[e], "w" + id);
                         break;
                     }
-                    case kErPark: put(S.ep[e], a); break;
+                    case kErPark:
+                        put(S.ep[e], a);
+                        if (drop_pair) s += "  }\n";
+                        break;
                     case kErFinish:
                         put(S.ed0[e], "pft3(" + a + ", v" + id + ")");
                         put(S.epd[e], "pft3(v" + id + ", " + a + ")");
+                        if (drop_pair) s += "  }\n";
                         break;
                     default: break;
                 }
