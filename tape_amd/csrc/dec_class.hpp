@@ -147,6 +147,7 @@ struct DecClassGenOpt {
     bool fuse = true;   // dec_prog_fuse_type1
     bool pairs = true;  // dec_prog fuse_pairs
     bool tu_perm = true;  // type-1 coefficient as a v_perm table product (false: xtime chain)
+    bool drop_branch = true;  // out_st skips a dropped row with a uniform branch (false: range check)
     bool drop_pairs = false;  // decode: skip column-0 pairs whose nodes are both parity (slower: the
                               // 420 uniform branches per kernel cost more scheduling than the rows)
 };
@@ -295,7 +296,8 @@ inline std::string dec_class_source(const ClayHost &h, int id, uint8_t t_u, DecP
             if (loc == kLocNone) return;
             if (lty(loc) == kLocStage) {
                 const uint32_t it = S.out[lix(loc)];
-                emit("  T.out_st(ob%u, %s, %s);\n", it & 0xffu, poff((it >> 8) & 0xffu).c_str(), v.c_str());
+                emit("  T.%s(ob%u, %s, %s);\n", opt.drop_branch ? "out_st" : "out_st_oob", it & 0xffu,
+                     poff((it >> 8) & 0xffu).c_str(), v.c_str());
             } else if (lty(loc) == kLocSlot || small) {
                 emit("  T.lds_st(%u, %s);\n", lrow(loc), v.c_str());
             } else {

@@ -115,6 +115,11 @@ struct CTile {
     // word across the end of the stripe's output share is written byte by byte
     __device__ __forceinline__ void out_st(u32 ob, u32 po, u32 v) const {
         if (ob == kDropBase) return;  // uniform: a column-0 parity node's row is not output
+        out_st_oob(ob, po, v);
+    }
+    // the same without the uniform skip: a dropped row's store goes past the buffer's range and
+    // the range check discards it (measurement variant, gen_dec_class TEC_GEN_DROP_BRANCH=0)
+    __device__ __forceinline__ void out_st_oob(u32 ob, u32 po, u32 v) const {
         const u32 o = ob + po + vcol;
         if (full) {  // uniform: every data row of the stripe lies inside its output share
             __builtin_amdgcn_raw_buffer_store_b32(v, rs_out, (int)o, 0, 2);
